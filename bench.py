@@ -1,0 +1,324 @@
+#!/usr/bin/env python3
+"""bench.py -- decoded MB/s of 2048x1536 8-bit grayscale frames on MI355X.
+
+BASELINE.json metric: "decoded MB/s (and Mpixels/s) at 2048x1536 grayscale,
+1/2/4/8 GPU + CPU ref". MB = 1e6 bytes of decoded raster (1 byte per pixel, so
+Mpixel/s is the same number).
+
+A step is one pass of the hot path over one batch of input: by default
+(--workload frame, BASELINE config 2) one kernel launch that decodes one
+2048x1536 frame per GPU. Inputs are resident in HBM before timing starts: each
+rank holds --frames distinct block-shuffled BigBridge frames (the reference's
+own TEST_IMAGE4 asset; every shuffle shares one canonical table) and step i
+decodes frame i mod --frames, so repeated steps do not hit a warm cache
+(64 frames x 5.3 MB > the 256 MiB Infinity Cache). The K timed launches are
+captured in one hipGraph (HIP stream capture through torch.cuda.CUDAGraph) and
+replayed. Per-launch kernel durations (the roofline's denominator) come from HIP
+event pairs on the launch stream around the same launches issued eagerly right
+after the timed region (HIP does not time events recorded inside a capture).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
+per GPU; rank 0 broadcasts the shared T1||T2 table over RCCL (xGMI) once; frames
+are sharded (each rank decodes its own), no collective on the data path;
+value = all frames decoded / max-over-ranks wall time ("weak" scaling).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded MB/s (and Mpixels/s) at 2048×1536 grayscale, 1/2/4/8 GPU + CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=["frame", "batch", "tile8192"], default="frame")
+    ap.add_argument("--frames", type=int, default=64, help="distinct resident frames per rank")
+    ap.add_argument("--batch", type=int, default=64, help="frames per launch for --workload batch")
+    ap.add_argument("--no-extras", action="store_true", help="skip the batch/tile side measurements")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
+    return ap.parse_args(argv)
+
+
+# --------------------------------------------------------------------------------------
+def encode_many(imgs, threads=8):
+    import metalhuffman_amd as mh
+    with cf.ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL
+        return list(ex.map(mh.encode_frame, imgs))
+
+
+def algo_bytes(efs, t2_bytes: int) -> int:
+    """Algorithmic HBM bytes of one launch: payload codes +
+    block offsets + decoded raster per frame, T1 + T2 once per launch."""
+    per = sum(ef.payload_bytes + 4 * ef.n_blocks + ef.width * ef.height for ef in efs)
+    return per + 512 + t2_bytes
+
+
+class Workload:
+    """A set of launches (one DeviceFrames each) cycled over by the steps."""
+
+    def __init__(self, name, launches, tables, pixels_per_launch, bytes_per_launch, device):
+        from metalhuffman_amd import decoder as D
+        self.D = D
+        self.name = name
+        self.launches = launches
+        self.tables = tables
+        self.pixels = pixels_per_launch
+        self.bytes = bytes_per_launch
+        self.device = device
+        self.outs = [torch.empty((f.n_frames, f.height, (f.width + 7) // 8 * 8), dtype=torch.uint8,
+                                 device=device) for f in launches]
+
+    def launch(self, i):
+        j = i % len(self.launches)
+        self.D.decode(self.launches[j], self.tables, self.outs[j])
+
+    def run(self, steps, warmup, use_graph=True, world=1):
+        """Timed region: `steps` launches (one hipGraph replay, or eager), bracketed by
+        barrier + synchronize; wall = max over ranks.
+        Kernel durations: the same `steps` launches issued eagerly right after, each
+        bracketed by a pair of HIP events on the launch stream (HIP cannot record
+        timing events inside stream capture).
+        -> (wall_s, gpu_region_ms, per-launch kernel ms list)."""
+        dev = self.device
+        for i in range(warmup):
+            self.launch(i)
+        torch.cuda.synchronize(dev)
+        graph = None
+        if use_graph:
+            try:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    for i in range(steps):
+                        self.launch(i)
+                graph.replay()  # first replay off the clock (instantiation effects)
+                torch.cuda.synchronize(dev)
+            except Exception as e:  # pragma: no cover - fall back to eager launches
+                print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
+                graph = None
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r0.record()
+        if graph is not None:
+            graph.replay()
+        else:
+            for i in range(steps):
+                self.launch(i)
+        r1.record()
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([wall], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            wall = float(t.item())
+        region_ms = r0.elapsed_time(r1)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for i in range(steps):
+            ev[i][0].record()
+            self.launch(i)
+            ev[i][1].record()
+        torch.cuda.synchronize(dev)
+        kms = [a.elapsed_time(b) for a, b in ev]
+        return wall, region_ms, kms
+
+
+def roofline(bytes_per_launch, kernel_ms):
+    avg_s = float(np.mean(kernel_ms)) * 1e-3
+    ach = bytes_per_launch / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel_us_avg": round(avg_s * 1e6, 3), "kernel_us_median": round(float(np.median(kernel_ms)) * 1e3, 3),
+            "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+
+
+def cpu_baseline(efs, threads):
+    """The reference's CPU decode (HuffmanUtil::decodeHuffmanBitsFromTables,
+    Shared/HuffmanUtil.cpp:830-1046) restated in oracle/ (kind 'port'), timed on
+    this host: single thread and frame-parallel on `threads` threads."""
+    from oracle import oracle as O
+    O.build()
+    t1, t2 = efs[0].tables()
+    nsym = efs[0].n_blocks * 64
+    bufs = [ef.codes for ef in efs]
+    one = O.time_decode_frames(t1, t2, nsym, bufs[:1], 1, reps=16)
+    mb1 = 16 * efs[0].width * efs[0].height / one / 1e6
+    reps = max(1, int(round(1.0 * mb1 * 1e6 * threads / (len(bufs) * efs[0].width * efs[0].height))))
+    multi = O.time_decode_frames(t1, t2, nsym, bufs, threads, reps=reps)
+    mbn = reps * len(bufs) * efs[0].width * efs[0].height / multi / 1e6
+    return {"value": round(mbn, 1), "unit": "MB/s", "cores": threads, "kind": "port",
+            "sample": f"{reps}x{len(bufs)} BigBridge-shuffle frames (2048x1536, 4.89 bit/sym), "
+                      f"frame-parallel on {threads} threads, {multi:.2f}s; oracle restatement of "
+                      f"HuffmanUtil.cpp:830-1046 (gcc -O2)",
+            "single_thread_MBps": round(mb1, 1), "cpu_model": _cpu_model(),
+            "host_nproc": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# --------------------------------------------------------------------------------------
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import metalhuffman_amd as mh
+    import metalhuffman_amd.build as B
+    if not os.path.exists(mh.LIB_PATH):
+        B.build()
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import dist as MD
+    from metalhuffman_amd import frames as F
+
+    bb = F.bigbridge()
+    # shared table: built on rank 0, broadcast over RCCL
+    t_bcast_us = None
+    if world > 1:
+        t1 = t2 = None
+        if rank == 0:
+            t1, t2 = mh.encode_frame(bb).tables()
+        torch.cuda.synchronize(dev)
+        tb = time.perf_counter()
+        d1, d2 = MD.broadcast_tables(t1, t2, src=0, device=dev)
+        torch.cuda.synchronize(dev)
+        t_bcast_us = (time.perf_counter() - tb) * 1e6
+        tables = D.DeviceTables(d1.clone(), d2.clone(), None)
+        tables.prepare_lut()
+    else:
+        t1, t2 = mh.encode_frame(bb).tables()
+        tables = D.DeviceTables.upload(t1, t2, dev)
+    t2_bytes = tables.table2.numel()
+
+    # this rank's resident frames (distinct block shuffles: one shared table)
+    seeds = [rank * args.frames + i for i in range(args.frames)]
+    efs = encode_many([F.block_shuffle(bb, s) for s in seeds])
+    for ef in efs:
+        assert np.array_equal(ef.canon, efs[0].canon)
+
+    def frame_workload():
+        launches = [D.DeviceFrames.pack([ef], dev) for ef in efs]
+        return Workload("frame", launches, tables, bb.size, algo_bytes(efs[:1], t2_bytes), dev)
+
+    def batch_workload(nb):
+        groups = [efs[i:i + nb] for i in range(0, len(efs), nb)]
+        groups = [g for g in groups if len(g) == nb] or [efs[:nb]]
+        launches = [D.DeviceFrames.pack(g, dev) for g in groups]
+        return Workload(f"batch{nb}", launches, tables, nb * bb.size, algo_bytes(groups[0], t2_bytes), dev)
+
+    def tile_workload():
+        base = F.mirror_tile(bb, 8192, 8192)
+        imgs = [base] + [F.block_shuffle(base, 100 + k) for k in range(2)]
+        tefs = encode_many(imgs, threads=3)
+        t1t, t2t = tefs[0].tables()
+        ttabs = D.DeviceTables.upload(t1t, t2t, dev)
+        launches = [D.DeviceFrames.pack([ef], dev) for ef in tefs]
+        return Workload("tile8192", launches, ttabs, base.size, algo_bytes(tefs[:1], ttabs.table2.numel()), dev)
+
+    if args.workload == "frame":
+        wl = frame_workload()
+        wdesc = "config2: one 2048x1536 BigBridge-derived frame per launch per GPU"
+    elif args.workload == "batch":
+        wl = batch_workload(args.batch)
+        wdesc = f"config4 shard: {args.batch} 2048x1536 frames per launch per GPU"
+    else:
+        wl = tile_workload()
+        wdesc = "config3: one 8192x8192 BigBridge mirror-tile per launch per GPU"
+
+    # parity guard: the timed path must produce the exact frames
+    wl.launch(0)
+    torch.cuda.synchronize(dev)
+    chk = wl.outs[0][0, :, : wl.launches[0].width].cpu().numpy()
+    ref_img = F.block_shuffle(bb, seeds[0]) if args.workload != "tile8192" else F.mirror_tile(bb, 8192, 8192)
+    if not np.array_equal(chk, ref_img) and not os.environ.get("MH_LIB"):
+        raise SystemExit("bench: decoded frame differs from the encoder input")
+
+    wall, region_ms, kms = wl.run(args.steps, args.warmup, use_graph=not args.no_graph, world=world)
+    per_step = wall / args.steps
+    value = world * wl.pixels / per_step / 1e6
+
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "MB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_step * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: block-shuffled BigBridge.png (reference TEST_IMAGE4 asset), "
+                f"{args.frames} distinct frames resident per GPU, shared canonical table",
+        "config": {"workload": wdesc, "width": int(ref_img.shape[1]), "height": int(ref_img.shape[0]),
+                   "frames_per_step_per_gpu": int(wl.launches[0].n_frames),
+                   "parallelism": f"frame-sharded x{world}", "launch": "hipGraph" if not args.no_graph else "eager"},
+        "mpixels_per_s": round(value, 1),
+        "roofline": roofline(wl.bytes, kms),
+        "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
+    }
+    if t_bcast_us is not None:
+        result["table_broadcast_us"] = round(t_bcast_us, 1)
+
+    if world == 1 and rank == 0 and not args.no_extras:
+        extras = {}
+        for name, make, steps in (("batch64", lambda: batch_workload(args.batch), 20),
+                                  ("tile8192", tile_workload, 20)):
+            if name.startswith("batch") and args.workload == "batch":
+                continue
+            if name == "tile8192" and args.workload == "tile8192":
+                continue
+            w2 = make()
+            wall2, reg2, kms2 = w2.run(steps, 3, use_graph=not args.no_graph)
+            extras[name] = {"value_MBps": round(w2.pixels / (wall2 / steps) / 1e6, 1),
+                            "ms_per_step": round(wall2 / steps * 1e3, 4),
+                            "gpu_region_ms_per_step": round(reg2 / steps, 4),
+                            "roofline": roofline(w2.bytes, kms2)}
+            del w2
+        result["extras"] = extras
+
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(efs[: min(len(efs), 32)], args.cpu_threads)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

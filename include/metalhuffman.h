@@ -1,0 +1,193 @@
+/*
+ * metalhuffman.h -- C-ABI of the MI355X-native Huffman block decoder.
+ *
+ * Drop-in boundary for the per-frame decode path of mdejong/MetalHuffman.
+ * The reference binds five buffers to its Metal fragment shaders
+ * (Shared/AAPLRenderer.m:1233-1253, slot enum Shared/AAPLShaderTypes.h:32-38):
+ *   [0] blockStartBitOffsets  u32[NB]             (AAPLRenderer.m:1237, :863-864, :672-685)
+ *   [1] huffBuff              u8[codes + 2 pad]   (AAPLRenderer.m:1243, :576-585)
+ *   [2] huffSymbolTable1      HuffLookupSymbol[256] (AAPLRenderer.m:1247, :657)
+ *   [3] huffSymbolTable2      HuffLookupSymbol[(k+1)*256] (AAPLRenderer.m:1250, :660)
+ *   [4] dims uniform          {u16 width, height, blockWidth, blockHeight}
+ *                             (AAPLShaderTypes.h:89-95, AAPLRenderer.m:1253, :768-775)
+ * mh_decode() takes exactly those buffers (device pointers) and replaces the five
+ * huffFragmentShaderB8W12/B8W16 passes, the 16-slice blit and the
+ * cropAndGrayscaleFromTexturesFragmentShader reorder (AAPLShaders.metal:127-518,
+ * AAPLRenderer.m:1192-1678) with one kernel launch that writes the W x H 8-bit
+ * raster directly. The decoded value is the reference output texture's B byte.
+ *
+ * The producer side (mh_encode_*, mh_build_tables, ...) mirrors the reference's
+ * HuffmanUtil statics / Huffman ObjC facade (Shared/HuffmanUtil.hpp:22-100,
+ * Shared/Huffman.h:9-77) without module state: every call is reentrant.
+ *
+ * Conventions: plain pointers and sizes; `stream` is a hipStream_t (NULL = the
+ * default stream); device pointers are marked d_. The library never allocates
+ * on a decode call; tables are read-only during a decode. Every entry point
+ * returns MH_OK (0) or a negative MH_ERR_* code; decode calls never modify the
+ * output for a valid stream.
+ */
+#ifndef METALHUFFMAN_H
+#define METALHUFFMAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_VERSION_MAJOR 0
+#define MH_VERSION_MINOR 1
+
+/* --- status codes (the reference only asserts: HuffmanEncoder.cpp:131,
+ *     AAPLRenderer.m:199,215,721) --------------------------------------- */
+#define MH_OK 0
+#define MH_ERR_INVALID_ARG (-1)   /* NULL pointer, zero size, bad flags          */
+#define MH_ERR_DIMS (-2)          /* dims inconsistent or above the u16 limits   */
+#define MH_ERR_CODE_TOO_LONG (-3) /* Huffman depth > 16 (ref: assert codei < 16) */
+#define MH_ERR_CAPACITY (-4)      /* caller buffer too small                     */
+#define MH_ERR_TABLE (-5)         /* table2 smaller than 256 or not 256-aligned  */
+#define MH_ERR_ALIGN (-6)         /* codes not 16-byte aligned / pitch % 8 != 0  */
+#define MH_ERR_HIP (-7)           /* HIP runtime error (launch / no device)      */
+#define MH_ERR_EMPTY (-8)         /* no symbols to encode                        */
+
+/* --- constants (Shared/AAPLShaderTypes.h:109-123) --------------------- */
+#define MH_BLOCK_DIM 8           /* HUFF_BLOCK_DIM                              */
+#define MH_TABLE1_NUM_BITS 8     /* HUFF_TABLE1_NUM_BITS                        */
+#define MH_TABLE2_NUM_BITS 8     /* HUFF_TABLE2_NUM_BITS                        */
+#define MH_TABLE1_SIZE 256       /* HUFF_TABLE1_SIZE                            */
+#define MH_TABLE2_SIZE 256       /* HUFF_TABLE2_SIZE (entries per subtable)     */
+#define MH_TABLE2_MAX_ENTRIES (257 * 256)
+#define MH_MAX_DIM 65535         /* u16 fields of the dims uniform              */
+#define MH_CODES_PAD 4           /* zero bytes after the payload: 2 from the
+                                    encoder (HuffmanEncoder.cpp:377-378) + 2 from
+                                    the renderer (AAPLRenderer.m:576-585)       */
+
+/* decode flags */
+#define MH_FLAG_NO_DELTA 0x1u    /* IMPL_DELTAS_BEFORE_HUFF_ENCODING off
+                                    (AAPLShaders.metal:263-265): emit symbols raw */
+
+/* Shared/HuffmanLookupSymbol.h:7-10: 2-byte entry. In T1, bitWidth == 0 marks
+ * an escape whose `symbol` is the T2 subtable index (HuffmanUtil.cpp:639-646). */
+typedef struct {
+  uint8_t symbol;
+  uint8_t bitWidth;
+} mh_lookup_symbol;
+
+/* Shared/AAPLShaderTypes.h:89-95 RenderTargetDimensionsAndBlockDimensionsUniform,
+ * widened to u32 (values must still fit the reference's u16 fields). */
+typedef struct {
+  uint32_t width;
+  uint32_t height;
+  uint32_t block_width;  /* ceil(width / 8)  (AAPLRenderer.m:753-761) */
+  uint32_t block_height; /* ceil(height / 8) */
+} mh_dims;
+
+/* One frame, or a batch of frames that share one table pair and one size.
+ * Frame f's block offsets are d_block_offsets[f*NB .. f*NB+NB) (bit offsets
+ * relative to frame f's first code byte); its code bytes start at
+ * d_codes + frame_code_offsets[f] (16-byte aligned). */
+typedef struct {
+  const uint32_t *d_block_offsets;        /* slot [0], u32[n_frames * NB]      */
+  const uint8_t *d_codes;                 /* slot [1], 16-byte aligned          */
+  uint64_t codes_bytes;                   /* bytes readable at d_codes          */
+  const uint64_t *d_frame_code_offsets;   /* u64[n_frames + 1], or NULL when
+                                             n_frames == 1 (frame = whole buf) */
+  const mh_lookup_symbol *d_table1;       /* slot [2], 256 entries              */
+  const mh_lookup_symbol *d_table2;       /* slot [3], table2_entries entries   */
+  uint32_t table2_entries;                /* (k+1)*256, k = #subtables          */
+  const uint16_t *d_lut;                  /* optional: mh_prepare_lut() output,
+                                             NULL = derive it inside the kernel */
+  const uint8_t *d_block_init;            /* optional u8[n_frames*NB]: per-block
+                                             initial prev symbol
+                                             (IMPL_DELTAS_AND_INIT_ZERO_DELTA_...,
+                                             AAPLRenderer.m:449-473,
+                                             AAPLShaders.metal:324); NULL = 0  */
+  mh_dims dims;                           /* slot [4]                           */
+  uint32_t n_frames;
+  uint32_t flags;                         /* MH_FLAG_*                          */
+} mh_frame;
+
+/* ---------------------------------------------------------------------- */
+/* GPU decode (the hot path).                                              */
+
+/* Decode n_frames frames into d_out: frame f, row y starts at
+ * d_out + f*out_frame_stride + y*out_pitch; W bytes per row are written.
+ * out_pitch must be a multiple of 8 (the kernel stores 8-pixel block rows).
+ * Asynchronous on `stream`; one kernel launch. */
+int mh_decode(const mh_frame *frame, uint8_t *d_out, size_t out_pitch,
+              size_t out_frame_stride, void *stream);
+
+/* Bytes needed for the derived lookup table mh_prepare_lut() writes. */
+size_t mh_lut_bytes(void);
+
+/* Derive the decoder's 2^MH_LUT_BITS-entry first-level table from T1/T2 on the
+ * device (one small kernel). Rebuild only when the tables change, exactly as
+ * the reference builds T1/T2 once (AAPLRenderer.m:608). */
+int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_table2,
+                   uint32_t table2_entries, uint16_t *d_lut, void *stream);
+
+/* Number of LUT index bits used by the kernel (first-level lookup width). */
+int mh_lut_bits(void);
+
+/* ---------------------------------------------------------------------- */
+/* Host-side producer (CPU, reentrant). Outputs are byte-identical to the   */
+/* reference's C++ codec.                                                   */
+
+/* Util.m:233-323 splitIntoBlocksOfSize (zero pad). out: bw*bh*bdim*bdim bytes. */
+int mh_split_blocks(const uint8_t *img, uint32_t width, uint32_t height, uint32_t block_dim,
+                    uint8_t zero_value, uint8_t *out, size_t out_bytes);
+
+/* Inverse of mh_split_blocks: block order -> W x H raster (crop). */
+int mh_merge_blocks(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t block_dim,
+                    uint8_t *out, size_t out_pitch);
+
+/* HuffmanUtil::encodeSignedByteDeltas / decodeSignedByteDeltas
+ * (HuffmanUtil.cpp:1133-1145 -> :21-78), applied to n bytes; in == out allowed. */
+int mh_encode_signed_byte_deltas(const uint8_t *in, uint8_t *out, size_t n);
+int mh_decode_signed_byte_deltas(const uint8_t *in, uint8_t *out, size_t n);
+
+/* Upper bound of the codes bytes mh_encode_huffman / mh_encode_frame write. */
+uint64_t mh_codes_bound(uint64_t n_symbols);
+
+/* HuffmanUtil::encodeHuffman (HuffmanUtil.cpp:1051-1131 -> HuffmanEncoder::encode
+ * HuffmanEncoder.cpp:310-381): canonical header, MSB-first codes followed by the
+ * encoder's 2 zero bytes (*codes_len includes them) and the bit offset of every
+ * block_dim*block_dim-th symbol (n_symbols / (block_dim^2) entries). */
+int mh_encode_huffman(const uint8_t *symbols, uint64_t n_symbols, uint32_t block_dim,
+                      uint8_t canon_header[256], uint8_t *codes, uint64_t codes_cap,
+                      uint64_t *codes_len, uint32_t *block_bit_offsets);
+
+/* The renderer's whole producer step (AAPLRenderer.m:374-688) for one 8-bit
+ * gray frame: split into zero-padded 8x8 blocks, per-block deltas (unless
+ * MH_FLAG_NO_DELTA), encode, block offsets, and MH_CODES_PAD zero bytes of
+ * read-ahead after the payload (*codes_len includes them). codes_cap >=
+ * mh_codes_bound(NB*64) + 2. block_offsets: NB entries. block_init (optional,
+ * NB bytes): when non-NULL, the first delta of every block is moved into it
+ * and zeroed (IMPL_DELTAS_AND_INIT_ZERO_DELTA_BEFORE_HUFF_ENCODING,
+ * AAPLRenderer.m:449-473). */
+int mh_encode_frame(const uint8_t *gray, uint32_t width, uint32_t height, uint32_t flags,
+                    uint8_t canon_header[256], uint8_t *codes, uint64_t codes_cap,
+                    uint64_t *codes_len, uint32_t *block_offsets, uint8_t *block_init);
+
+/* huff_util.hpp:94-193 huff_generate_canonical_codes: left-justified u16 codes. */
+int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]);
+
+/* HuffmanUtil::parseCanonicalHeader + generateSplitLookupTables(8, 8, ...)
+ * (HuffmanUtil.cpp:270-310, :338-667), without module statics. table2 needs
+ * room for MH_TABLE2_MAX_ENTRIES entries; *table2_entries = (k+1)*256. */
+int mh_build_tables(const uint8_t canon_header[256], mh_lookup_symbol table1[256],
+                    mh_lookup_symbol *table2, uint32_t table2_cap, uint32_t *table2_entries);
+
+/* HuffmanUtil::generateLookupTable (HuffmanUtil.cpp:314-334): 65536 entries. */
+int mh_build_single_table(const uint8_t canon_header[256], mh_lookup_symbol table[65536]);
+
+/* ---------------------------------------------------------------------- */
+/* Utilities */
+const char *mh_error_string(int status);
+int mh_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* METALHUFFMAN_H */

@@ -1,0 +1,18 @@
+"""metalhuffman_amd -- MI355X-native Huffman block decoder (drop-in for the decode path
+of mdejong/MetalHuffman).
+
+  * include/metalhuffman.h          C-ABI (the drop-in boundary)
+  * csrc/mh_decode.hip              hand-written gfx950 decode kernel
+  * csrc/mh_host.cpp                host producer: encoder, canonical codes, T1/T2
+  * codec.Huffman                   the reference's `Huffman` facade (Shared/Huffman.h)
+  * decoder.decode / DeviceFrames   GPU decode of one frame or a batch
+  * dist                            frame sharding + table broadcast (RCCL / gloo)
+"""
+from ._native import EXPORTS, LIB_PATH, MH_CODES_PAD, MH_FLAG_NO_DELTA, MHError, lib
+from .codec import BLOCK_DIM, EncodedFrame, Huffman, block_grid, encode_frame, merge_blocks, split_blocks
+
+__all__ = [
+    "EXPORTS", "LIB_PATH", "MH_CODES_PAD", "MH_FLAG_NO_DELTA", "MHError", "lib", "BLOCK_DIM",
+    "EncodedFrame", "Huffman", "block_grid", "encode_frame", "merge_blocks", "split_blocks",
+]
+__version__ = "0.1.0"

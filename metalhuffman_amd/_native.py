@@ -1,0 +1,103 @@
+"""ctypes binding of libmetalhuffman_amd.so (the C-ABI in include/metalhuffman.h).
+
+The library is loaded from this package directory only. If it is missing the
+import fails loudly: there is no CPU fallback for the decode path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MH_LIB") or os.path.join(_PKG, "libmetalhuffman_amd.so")
+
+MH_OK = 0
+MH_FLAG_NO_DELTA = 0x1
+MH_CODES_PAD = 4
+MH_TABLE2_MAX_ENTRIES = 257 * 256
+MH_MAX_DIM = 65535
+
+# every symbol include/metalhuffman.h declares
+EXPORTS = (
+    "mh_decode", "mh_lut_bytes", "mh_prepare_lut", "mh_lut_bits", "mh_split_blocks",
+    "mh_merge_blocks", "mh_encode_signed_byte_deltas", "mh_decode_signed_byte_deltas",
+    "mh_codes_bound", "mh_encode_huffman", "mh_encode_frame", "mh_canonical_codes",
+    "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
+)
+
+
+class MHError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = lib().mh_error_string(status).decode() if _lib is not None else str(status)
+        super().__init__(f"{what}: {msg} (status {status})" if what else f"{msg} (status {status})")
+
+
+class mh_dims(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("block_width", ctypes.c_uint32), ("block_height", ctypes.c_uint32)]
+
+
+class mh_frame(ctypes.Structure):
+    _fields_ = [
+        ("d_block_offsets", ctypes.c_void_p),
+        ("d_codes", ctypes.c_void_p),
+        ("codes_bytes", ctypes.c_uint64),
+        ("d_frame_code_offsets", ctypes.c_void_p),
+        ("d_table1", ctypes.c_void_p),
+        ("d_table2", ctypes.c_void_p),
+        ("table2_entries", ctypes.c_uint32),
+        ("d_lut", ctypes.c_void_p),
+        ("d_block_init", ctypes.c_void_p),
+        ("dims", mh_dims),
+        ("n_frames", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: build it with `python -m metalhuffman_amd.build` "
+                "(the HIP decoder has no fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.mh_decode.argtypes = [ctypes.POINTER(mh_frame), _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]
+        L.mh_lut_bytes.restype = ctypes.c_size_t
+        L.mh_lut_bits.restype = ctypes.c_int
+        L.mh_prepare_lut.argtypes = [_vp, _vp, ctypes.c_uint32, _vp, _vp]
+        L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint8, _u8p, ctypes.c_size_t]
+        L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
+                                      ctypes.c_size_t]
+        L.mh_encode_signed_byte_deltas.argtypes = [_u8p, _u8p, ctypes.c_size_t]
+        L.mh_decode_signed_byte_deltas.argtypes = [_u8p, _u8p, ctypes.c_size_t]
+        L.mh_codes_bound.argtypes = [ctypes.c_uint64]
+        L.mh_codes_bound.restype = ctypes.c_uint64
+        L.mh_encode_huffman.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, _u8p, _u8p,
+                                        ctypes.c_uint64, _u64p, _u32p]
+        L.mh_encode_frame.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
+                                      _u8p, ctypes.c_uint64, _u64p, _u32p, _u8p]
+        L.mh_canonical_codes.argtypes = [_u8p, _u16p]
+        L.mh_build_tables.argtypes = [_u8p, _u8p, _u8p, ctypes.c_uint32, _u32p]
+        L.mh_build_single_table.argtypes = [_u8p, _u8p]
+        L.mh_error_string.argtypes = [ctypes.c_int]
+        L.mh_error_string.restype = ctypes.c_char_p
+        L.mh_device_count.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != MH_OK:
+        raise MHError(status, what)

@@ -1,0 +1,89 @@
+"""Build libmetalhuffman_amd.so in-tree (hipcc for gfx950 + g++ for the host codec).
+
+    python -m metalhuffman_amd.build            # incremental
+    python -m metalhuffman_amd.build --force
+
+The shared library lands next to this file so it travels with the repository
+snapshot to the GPU box; nothing is installed into site-packages.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "libmetalhuffman_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("MH_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = {
+    "mh_decode.o": ("mh_decode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+                                      "-Wall", "-c"]),
+    "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),
+}
+HEADERS = [os.path.join(ROOT, "include", "metalhuffman.h")]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    objs = []
+    for obj, (src, cmd) in SOURCES.items():
+        src_path = os.path.join(CSRC, src)
+        obj_path = os.path.join(BUILD, obj)
+        objs.append(obj_path)
+        if force or _stale(obj_path, [src_path] + HEADERS):
+            full = cmd + [src_path, "-o", obj_path]
+            if verbose:
+                print(" ".join(full), flush=True)
+            subprocess.run(full, check=True)
+    if force or _stale(LIB, objs):
+        full = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        if verbose:
+            print(" ".join(full), flush=True)
+        subprocess.run(full, check=True)
+    return LIB
+
+
+VARIANTS_DIR = os.path.join(PKG, "_variants")
+
+
+def build_variant(name: str, defines: list[str], verbose: bool = False) -> str:
+    """Experiment builds (A/B on the GPU): same sources, extra -D flags, loaded with
+    MH_LIB=<path>. Never the default library."""
+    os.makedirs(VARIANTS_DIR, exist_ok=True)
+    tmp = os.path.join(BUILD, f"variant_{name}")
+    os.makedirs(tmp, exist_ok=True)
+    objs = []
+    for obj, (src, cmd) in SOURCES.items():
+        o = os.path.join(tmp, obj)
+        subprocess.run(cmd + [f"-D{d}" for d in defines] + [os.path.join(CSRC, src), "-o", o], check=True)
+        objs.append(o)
+    out = os.path.join(VARIANTS_DIR, f"lib_{name}.so")
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    if verbose:
+        print(out)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args(argv)
+    print(build(force=args.force, verbose=True))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,201 @@
+"""Host-side producer API (CPU) -- the reference's `Huffman` facade without module state.
+
+Mirrors the class methods of Shared/Huffman.h:9-77 (ObjC) / HuffmanUtil statics
+(Shared/HuffmanUtil.hpp:22-100) with the same names and argument meaning, backed by
+the C++ codec in libmetalhuffman_amd.so (csrc/mh_host.cpp). Outputs are
+byte-identical to the reference encoder and table builder.
+
+Differences from the reference, by design:
+  * no module statics: parseCanonicalHeader returns the canonical codes instead of
+    stashing them (HuffmanUtil.cpp:87-102), and generateSplitLookupTables takes the
+    canonical header explicitly;
+  * errors raise MHError instead of assert() (e.g. a code deeper than 16 bits,
+    HuffmanEncoder.cpp:131);
+  * the CPU decoders (decodeHuffmanBits*) are not part of the product: the GPU
+    decoder is the decode path; the CPU restatement lives in oracle/ as the checker.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _p(a: np.ndarray, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def _u8(a) -> np.ndarray:
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(a), dtype=np.uint8)
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+BLOCK_DIM = 8
+
+
+def block_grid(width: int, height: int, block_dim: int = BLOCK_DIM) -> tuple[int, int]:
+    """AAPLRenderer.m:753-761: ceil(W/8) x ceil(H/8)."""
+    return -(-width // block_dim), -(-height // block_dim)
+
+
+@dataclasses.dataclass
+class EncodedFrame:
+    """One frame in the reference's buffer contract (AAPLRenderer.m:374-688)."""
+    width: int
+    height: int
+    canon: np.ndarray           # u8[256] canonical code lengths
+    codes: np.ndarray           # u8[payload + MH_CODES_PAD] (huffBuff, read-ahead included)
+    block_offsets: np.ndarray   # u32[NB] bit offset of every 8x8 block
+    block_init: Optional[np.ndarray] = None  # u8[NB] (INIT_ZERO_DELTA mode) or None
+    flags: int = 0
+
+    @property
+    def block_width(self) -> int:
+        return block_grid(self.width, self.height)[0]
+
+    @property
+    def block_height(self) -> int:
+        return block_grid(self.width, self.height)[1]
+
+    @property
+    def n_blocks(self) -> int:
+        return self.block_width * self.block_height
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.codes.size) - N.MH_CODES_PAD
+
+    def tables(self) -> tuple[np.ndarray, np.ndarray]:
+        return Huffman.generateSplitLookupTables(self.canon)
+
+
+class Huffman:
+    """Stateless mirror of the reference's `Huffman` class (Shared/Huffman.h)."""
+
+    # +parseCanonicalHeader: (Huffman.h:14, HuffmanUtil.cpp:270-310)
+    @staticmethod
+    def parseCanonicalHeader(canonData) -> np.ndarray:
+        canon = _u8(canonData)
+        if canon.size != 256:
+            raise ValueError("canonical header must be 256 bytes")
+        codes = np.zeros(256, np.uint16)
+        N.check(N.lib().mh_canonical_codes(_p(canon), _p(codes, _u16p)), "parseCanonicalHeader")
+        return codes
+
+    # +generateLookupTable:lookupTableNumEntries: (Huffman.h:18, HuffmanUtil.cpp:314-334)
+    @staticmethod
+    def generateLookupTable(canonData) -> np.ndarray:
+        canon = _u8(canonData)
+        table = np.zeros(65536 * 2, np.uint8)
+        N.check(N.lib().mh_build_single_table(_p(canon), _p(table)), "generateLookupTable")
+        return table
+
+    # +generateSplitLookupTables:table2NumBits:table1:table2: (Huffman.h:21-24,
+    # HuffmanUtil.cpp:338-667). Returns (T1, T2) as raw 2-byte-entry arrays.
+    @staticmethod
+    def generateSplitLookupTables(canonData, table1NumBits: int = 8, table2NumBits: int = 8):
+        if (table1NumBits, table2NumBits) != (8, 8):
+            # the reference's table sizes are the compile-time HUFF_TABLE{1,2}_SIZE
+            # (AAPLShaderTypes.h:120-123); only the 8/8 split is a valid contract
+            raise ValueError("only the 8+8 split (HUFF_TABLE1/2_NUM_BITS) is supported")
+        canon = _u8(canonData)
+        t1 = np.zeros(512, np.uint8)
+        t2 = np.zeros(N.MH_TABLE2_MAX_ENTRIES * 2, np.uint8)
+        ent = ctypes.c_uint32(0)
+        N.check(N.lib().mh_build_tables(_p(canon), _p(t1), _p(t2), N.MH_TABLE2_MAX_ENTRIES,
+                                        ctypes.byref(ent)), "generateSplitLookupTables")
+        return t1, t2[: 2 * ent.value].copy()
+
+    # +encodeHuffman:inNumBytes:outFileHeader:outCanonHeader:outHuffCodes:
+    #  outBlockBitOffsets:width:height:blockDim: (Huffman.h:62-70, HuffmanUtil.cpp:1051-1131)
+    @staticmethod
+    def encodeHuffman(inBytes, width: int, height: int, blockDim: int = BLOCK_DIM):
+        """-> (fileHeader, canonHeader, huffCodes, blockBitOffsets).
+
+        fileHeader is empty, as in the reference (HuffmanUtil.cpp:1073-1086 never
+        copies the encoder's header bytes out); huffCodes carries the encoder's
+        2 zero bytes of read-ahead."""
+        sym = _u8(inBytes)
+        if sym.size == 0:
+            raise N.MHError(-8, "encodeHuffman")
+        cap = int(N.lib().mh_codes_bound(sym.size))
+        canon = np.zeros(256, np.uint8)
+        codes = np.zeros(cap, np.uint8)
+        stride = blockDim * blockDim
+        offs = np.zeros(max(1, sym.size // stride), np.uint32)
+        ln = ctypes.c_uint64(0)
+        N.check(N.lib().mh_encode_huffman(_p(sym), sym.size, blockDim, _p(canon), _p(codes), cap,
+                                          ctypes.byref(ln), _p(offs, _u32p)), "encodeHuffman")
+        return (np.zeros(0, np.uint8), canon, codes[: ln.value].copy(),
+                offs[: sym.size // stride].copy())
+
+    # +encodeSignedByteDeltas: / +decodeSignedByteDeltas: (Huffman.h:72-76)
+    @staticmethod
+    def encodeSignedByteDeltas(data) -> np.ndarray:
+        a = _u8(data)
+        out = np.empty_like(a)
+        N.check(N.lib().mh_encode_signed_byte_deltas(_p(a), _p(out), a.size), "encodeSignedByteDeltas")
+        return out
+
+    @staticmethod
+    def decodeSignedByteDeltas(deltas) -> np.ndarray:
+        a = _u8(deltas)
+        out = np.empty_like(a)
+        N.check(N.lib().mh_decode_signed_byte_deltas(_p(a), _p(out), a.size), "decodeSignedByteDeltas")
+        return out
+
+    # snake_case aliases
+    parse_canonical_header = parseCanonicalHeader
+    generate_lookup_table = generateLookupTable
+    generate_split_lookup_tables = generateSplitLookupTables
+    encode_huffman = encodeHuffman
+    encode_signed_byte_deltas = encodeSignedByteDeltas
+    decode_signed_byte_deltas = decodeSignedByteDeltas
+
+
+def split_blocks(img: np.ndarray, block_dim: int = BLOCK_DIM, zero_value: int = 0) -> np.ndarray:
+    """Util.m:233-323 splitIntoBlocksOfSize (zero padded) -> block-order bytes."""
+    img = _u8(img)
+    h, w = img.shape
+    bw, bh = block_grid(w, h, block_dim)
+    out = np.empty(bw * bh * block_dim * block_dim, np.uint8)
+    N.check(N.lib().mh_split_blocks(_p(img), w, h, block_dim, zero_value, _p(out), out.size),
+            "split_blocks")
+    return out
+
+
+def merge_blocks(blocks: np.ndarray, width: int, height: int, block_dim: int = BLOCK_DIM) -> np.ndarray:
+    blocks = _u8(blocks)
+    out = np.empty((height, width), np.uint8)
+    N.check(N.lib().mh_merge_blocks(_p(blocks), width, height, block_dim, _p(out), width),
+            "merge_blocks")
+    return out
+
+
+def encode_frame(gray: np.ndarray, flags: int = 0, init_zero_delta: bool = False) -> EncodedFrame:
+    """The renderer's producer step (AAPLRenderer.m:374-688) for one 8-bit frame."""
+    gray = _u8(gray)
+    if gray.ndim != 2:
+        raise ValueError("expected a 2-D uint8 image")
+    h, w = gray.shape
+    bw, bh = block_grid(w, h)
+    nb = bw * bh
+    cap = int(N.lib().mh_codes_bound(nb * 64)) + 2
+    canon = np.zeros(256, np.uint8)
+    codes = np.zeros(cap, np.uint8)
+    offs = np.zeros(nb, np.uint32)
+    init = np.zeros(nb, np.uint8) if init_zero_delta else None
+    ln = ctypes.c_uint64(0)
+    N.check(N.lib().mh_encode_frame(_p(gray), w, h, flags, _p(canon), _p(codes), cap, ctypes.byref(ln),
+                                    _p(offs, _u32p), _p(init) if init is not None else None),
+            "encode_frame")
+    return EncodedFrame(w, h, canon, codes[: ln.value].copy(), offs, init, flags)

@@ -1,0 +1,157 @@
+"""GPU decode path: torch device tensors in, W x H uint8 raster out, via mh_decode().
+
+This is the host-side mirror of the reference renderer's decode contract
+(Shared/AAPLRenderer.m:1192-1678): the same five buffers (block offsets, huffBuff,
+T1, T2, dims) are uploaded once (the renderer's MTLBuffers, :576-667) and every
+decode is one launch of the HIP kernel in csrc/mh_decode.hip. PyTorch is only the
+device-memory / stream plumbing; nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .codec import EncodedFrame, block_grid
+
+ALIGN = 16  # frame code starts inside a packed batch (16-byte buffer loads)
+
+
+def _dev(device) -> torch.device:
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise RuntimeError("the MI355X decoder needs a HIP device (torch 'cuda' on ROCm)")
+    return d
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream], device: torch.device) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+@dataclasses.dataclass
+class DeviceTables:
+    """T1/T2 (+ the derived LDS table) resident on one device."""
+    table1: torch.Tensor     # u8[512]
+    table2: torch.Tensor     # u8[2 * entries]
+    lut: Optional[torch.Tensor]  # u8[mh_lut_bytes()] from mh_prepare_lut, or None
+
+    @property
+    def table2_entries(self) -> int:
+        return self.table2.numel() // 2
+
+    @classmethod
+    def upload(cls, t1: np.ndarray, t2: np.ndarray, device="cuda", prepare_lut: bool = True,
+               stream: Optional[torch.cuda.Stream] = None) -> "DeviceTables":
+        dev = _dev(device)
+        d1 = torch.from_numpy(np.ascontiguousarray(t1, np.uint8)).to(dev)
+        d2 = torch.from_numpy(np.ascontiguousarray(t2, np.uint8)).to(dev)
+        tabs = cls(d1, d2, None)
+        if prepare_lut:
+            tabs.prepare_lut(stream)
+        return tabs
+
+    def prepare_lut(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        dev = self.table1.device
+        lut = torch.empty(int(N.lib().mh_lut_bytes()), dtype=torch.uint8, device=dev)
+        N.check(N.lib().mh_prepare_lut(self.table1.data_ptr(), self.table2.data_ptr(),
+                                       self.table2_entries, lut.data_ptr(),
+                                       _stream_ptr(stream, dev)), "mh_prepare_lut")
+        self.lut = lut
+
+
+@dataclasses.dataclass
+class DeviceFrames:
+    """n frames of one size that share one table pair, packed for mh_decode."""
+    width: int
+    height: int
+    n_frames: int
+    block_offsets: torch.Tensor          # u32 as int32[n * NB]
+    codes: torch.Tensor                  # u8[total]
+    frame_code_offsets: Optional[torch.Tensor]  # int64[n + 1] (None for one frame)
+    block_init: Optional[torch.Tensor] = None   # u8[n * NB]
+    flags: int = 0
+    code_bytes: int = 0                  # payload bytes (sum over frames, pad excluded)
+
+    @property
+    def n_blocks(self) -> int:
+        bw, bh = block_grid(self.width, self.height)
+        return bw * bh
+
+    @classmethod
+    def pack(cls, frames: Sequence[EncodedFrame], device="cuda") -> "DeviceFrames":
+        """Upload frames (host arrays) into one packed device batch."""
+        dev = _dev(device)
+        if not frames:
+            raise ValueError("no frames")
+        w, h, fl = frames[0].width, frames[0].height, frames[0].flags
+        for f in frames:
+            if (f.width, f.height, f.flags) != (w, h, fl):
+                raise ValueError("a batch holds frames of one size and one format")
+            if not np.array_equal(f.canon, frames[0].canon):
+                raise ValueError("a batch shares one canonical table")
+        starts = [0]
+        for f in frames:
+            starts.append(starts[-1] + ((f.codes.size + ALIGN - 1) // ALIGN) * ALIGN)
+        packed = np.zeros(starts[-1], np.uint8)
+        for f, s in zip(frames, starts):
+            packed[s: s + f.codes.size] = f.codes
+        offs = np.concatenate([f.block_offsets for f in frames]).astype(np.uint32)
+        init = None
+        if frames[0].block_init is not None:
+            init = torch.from_numpy(np.concatenate([f.block_init for f in frames])).to(dev)
+        fco = None
+        if len(frames) > 1:
+            fco = torch.tensor(starts, dtype=torch.int64, device=dev)
+        return cls(w, h, len(frames), torch.from_numpy(offs.view(np.int32)).to(dev),
+                   torch.from_numpy(packed).to(dev), fco, init, fl,
+                   sum(f.payload_bytes for f in frames))
+
+
+def _frame_struct(frames: DeviceFrames, tables: DeviceTables) -> N.mh_frame:
+    bw, bh = block_grid(frames.width, frames.height)
+    fr = N.mh_frame()
+    fr.d_block_offsets = frames.block_offsets.data_ptr()
+    fr.d_codes = frames.codes.data_ptr()
+    fr.codes_bytes = frames.codes.numel()
+    fr.d_frame_code_offsets = (frames.frame_code_offsets.data_ptr()
+                               if frames.frame_code_offsets is not None else None)
+    fr.d_table1 = tables.table1.data_ptr()
+    fr.d_table2 = tables.table2.data_ptr()
+    fr.table2_entries = tables.table2_entries
+    fr.d_lut = tables.lut.data_ptr() if tables.lut is not None else None
+    fr.d_block_init = frames.block_init.data_ptr() if frames.block_init is not None else None
+    fr.dims = N.mh_dims(frames.width, frames.height, bw, bh)
+    fr.n_frames = frames.n_frames
+    fr.flags = frames.flags
+    return fr
+
+
+def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tensor] = None,
+           stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """Decode every frame into out[n, H, pitch] (pitch = W rounded up to 8)."""
+    dev = frames.codes.device
+    if tables.table1.device != dev:
+        raise ValueError("tables and frames must live on the same device")
+    pitch = (frames.width + 7) // 8 * 8
+    if out is None:
+        out = torch.empty((frames.n_frames, frames.height, pitch), dtype=torch.uint8, device=dev)
+    if out.dtype != torch.uint8 or not out.is_contiguous() or out.shape[-2:] != (frames.height, pitch):
+        raise ValueError(f"out must be contiguous uint8 [n, {frames.height}, {pitch}]")
+    fr = _frame_struct(frames, tables)
+    N.check(N.lib().mh_decode(ctypes.byref(fr), out.data_ptr(), pitch, frames.height * pitch,
+                              _stream_ptr(stream, dev)), "mh_decode")
+    return out
+
+
+def decode_frames(encoded: Sequence[EncodedFrame], device="cuda") -> np.ndarray:
+    """Convenience: upload, decode, copy back; returns [n, H, W] uint8 on the host."""
+    t1, t2 = encoded[0].tables()
+    tabs = DeviceTables.upload(t1, t2, device)
+    frames = DeviceFrames.pack(encoded, device)
+    out = decode(frames, tabs)
+    return out[..., : frames.width].cpu().numpy()

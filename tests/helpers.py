@@ -1,0 +1,54 @@
+"""Shared helpers for the test suite (CPU and GPU)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden() -> dict:
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+def image_from_block_deltas(deltas: np.ndarray, width: int, height: int) -> np.ndarray:
+    """Integrate per-block deltas (block order, 64 per block) into a raster whose
+    producer step (split + per-block delta) yields exactly `deltas`.
+    width and height must be multiples of 8 (no pad region to reproduce)."""
+    assert width % 8 == 0 and height % 8 == 0
+    bw, bh = width // 8, height // 8
+    d = deltas.reshape(bh * bw, 64).astype(np.uint16)
+    vals = (np.cumsum(d, axis=1) & 0xFF).astype(np.uint8)
+    return np.ascontiguousarray(vals.reshape(bh, bw, 8, 8).transpose(0, 2, 1, 3).reshape(height, width))
+
+
+def fibonacci_deltas(n_symbols: int, total: int, seed: int = 0) -> np.ndarray:
+    """A delta stream whose histogram is Fibonacci-shaped over `n_symbols` symbols
+    (deepest code = n_symbols - 1 bits), shuffled."""
+    fib = [1, 1]
+    while len(fib) < n_symbols:
+        fib.append(fib[-1] + fib[-2])
+    fib = np.array(fib[:n_symbols], dtype=np.int64)
+    reps = max(1, total // int(fib.sum()))
+    counts = fib * reps
+    syms = np.repeat(np.arange(n_symbols, dtype=np.uint8)[::-1], counts)
+    out = np.zeros(total, np.uint8)
+    out[: min(total, syms.size)] = syms[:total]
+    np.random.default_rng(seed).shuffle(out)
+    return out
+
+
+def long_span_deltas(width: int, height: int, seed: int = 0) -> np.ndarray:
+    """Mostly-zero deltas with every rare symbol packed into the FIRST tile
+    (64 blocks): that tile's code span exceeds the kernel's LDS window and takes the
+    global-memory path, while every code stays <= 16 bits."""
+    nb = (width // 8) * (height // 8)
+    d = np.zeros(nb * 64, np.uint8)
+    r = np.random.default_rng(seed)
+    first = 64 * 64
+    rare = r.integers(1, 256, size=first, dtype=np.uint8)
+    d[:first] = rare
+    return d
