@@ -59,16 +59,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
 VARIANTS_DIR = os.path.join(PKG, "_variants")
 
 
-def build_variant(name: str, defines: list[str], verbose: bool = False) -> str:
-    """Experiment builds (A/B on the GPU): same sources, extra -D flags, loaded with
-    MH_LIB=<path>. Never the default library."""
+def build_variant(name: str, defines: list[str], verbose: bool = False,
+                  decode_src: str | None = None) -> str:
+    """Experiment builds (A/B on the GPU): same sources (or another mh_decode.hip),
+    extra -D flags, loaded with MH_LIB=<path>. Never the default library."""
     os.makedirs(VARIANTS_DIR, exist_ok=True)
     tmp = os.path.join(BUILD, f"variant_{name}")
     os.makedirs(tmp, exist_ok=True)
     objs = []
     for obj, (src, cmd) in SOURCES.items():
         o = os.path.join(tmp, obj)
-        subprocess.run(cmd + [f"-D{d}" for d in defines] + [os.path.join(CSRC, src), "-o", o], check=True)
+        path = decode_src if (decode_src and src == "mh_decode.hip") else os.path.join(CSRC, src)
+        subprocess.run(cmd + [f"-D{d}" for d in defines] + [f"-I{CSRC}", path, "-o", o], check=True)
         objs.append(o)
     out = os.path.join(VARIANTS_DIR, f"lib_{name}.so")
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs, check=True)

@@ -34,6 +34,12 @@ namespace {
 #ifndef MH_DIAG_BROADCAST_LUT   // diagnostic builds only: LUT index forced to 0 (wrong output)
 #define MH_DIAG_BROADCAST_LUT 0
 #endif
+#ifndef MH_MIN_WAVES_PER_EU     // register cap: 6 waves/SIMD = what the LDS budget admits
+#define MH_MIN_WAVES_PER_EU 6
+#endif
+#ifndef MH_ROW_UNROLL           // 8: straight-line decode, so vmcnt can count the row stores
+#define MH_ROW_UNROLL 8
+#endif
 #ifndef MH_NT_STORE
 #define MH_NT_STORE 1
 #endif
@@ -63,6 +69,7 @@ struct DecodeArgs {
   uint8_t *out;
   uint64_t out_pitch;
   uint64_t out_frame_stride;
+  uint32_t out_frame_bytes;    // H * pitch (< 2^32): range of the per-frame store descriptor
   uint32_t t2_entries;
   uint32_t w, h, bw, bh, nb;
   uint32_t tiles_per_frame, total_tiles;
@@ -130,13 +137,6 @@ struct LdsWords {
   const uint32_t *w;
   __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i]; }
 };
-struct GlobalWords {  // fallback when a tile's span exceeds the LDS window
-  __amdgpu_buffer_rsrc_t rsrc;
-  uint32_t base;
-  __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
-    return bswap32(__builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(base + 4u * i), 0, 0));
-  }
-};
 
 // byte-insert selectors for v_perm_b32: put S0.byte0 at byte J, keep S1's others
 __device__ __forceinline__ constexpr uint32_t ins_sel(int j) {
@@ -148,11 +148,11 @@ __shared__ __attribute__((aligned(16))) uint8_t s_stage[kMaxWavesPerWG * kStageB
 __shared__ uint32_t s_p0;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
-// (cursor advance, delta fold); rows are stored as they complete.
+// (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
 template <bool kDelta, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_t prev,
-                                             bool store, uint8_t *dst, uint64_t pitch,
-                                             uint32_t cols, uint32_t rows) {
+                                             __amdgpu_buffer_rsrc_t out, uint32_t row0,
+                                             uint32_t pitch, bool dead) {
   uint32_t wi = p >> 5;
   uint32_t sh = p & 31u;
   uint32_t hi = src(wi);
@@ -190,7 +190,11 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
     nw = src(wi);                                                                   \
   }
 
+#if MH_ROW_UNROLL == 8
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (uint32_t r = 0; r < 8; ++r) {
     uint32_t o0 = 0, o1 = 0;
     if (r) MH_REFILL();
@@ -205,98 +209,294 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
     MH_REFILL();
     MH_STEP(2, o1);
     MH_STEP(3, o1);
-    if (store && r < rows) {
-      uint8_t *row = dst + (uint64_t)r * pitch;
-      if (cols == 8) {
-        if (MH_NT_STORE)
-          __builtin_nontemporal_store(((uint64_t)o1 << 32) | o0, reinterpret_cast<uint64_t *>(row));
-        else
-          *reinterpret_cast<uint2 *>(row) = make_uint2(o0, o1);
-      } else {  // right-edge block of a width that is not a multiple of 8 (crop)
-        const uint64_t v = ((uint64_t)o1 << 32) | o0;
-#pragma unroll
-        for (uint32_t x = 0; x < 7; ++x)
-          if (x < cols) row[x] = (uint8_t)(v >> (8 * x));
-      }
+    // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
+    // block and rows below the frame use offsets outside the descriptor's range,
+    // which the hardware drops. A right-edge block writes its 8 bytes into the
+    // row's pitch padding (pitch >= round_up(W, 8)).
+    {
+      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+      v2u32 v;
+      v.x = o0;
+      v.y = o1;
+      const uint32_t off = dead ? 0xFFFFFFF0u : row0 + r * pitch;
+      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
     }
   }
 #undef MH_STEP
 #undef MH_REFILL
 }
 
+constexpr int kStageChunks = (kStageBytes / 16 + 63) / 64;  // 16-B chunks per lane (5)
+
+// Buffer descriptors from provably wave-uniform inputs (readfirstlane), so hipcc
+// does not wrap each buffer op in a waterfall loop (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// A tile's header loads (issued one tile ahead; all VMEM so that no scalar load
+// is pending in lgkmcnt while the decode waits on LDS reads).
+struct TileHdr {
+  uint32_t tile;      // wave-uniform; >= total_tiles: no tile
+  uint32_t off;       // this lane's block start bit
+  uint32_t nxt;       // next block's start bit (this lane's block end)
+  uint32_t fo_lo, fo_hi;  // lanes 0/1: frame_off[f], frame_off[f+1]
+  uint32_t init;      // per-block initial prev (block_init) or 0
+};
+
+__device__ __forceinline__ void hdr_issue(const DecodeArgs &a, uint32_t tile, uint32_t lane,
+                                          TileHdr &h) {
+  // Branch-free: absent arrays (frame_off / block_init == NULL) get descriptors
+  // with zero records, whose loads return 0 without touching memory; a past-the-end
+  // tile reads through zero-record descriptors too. Unconditional loads keep the
+  // compiler from waiting on the span prefetch to re-zero these registers.
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  const bool live = tile < a.total_tiles;
+  const uint32_t f = live ? tile / a.tiles_per_frame : 0u;
+  const uint32_t b = (live ? (tile - f * a.tiles_per_frame) * 64u : 0u) + lane;
+  h.tile = tile;
+  const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(a.offsets + (uint64_t)f * a.nb, live ? a.nb * 4u : 0u);
+  h.off = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(b * 4u), 0, 0);
+  h.nxt = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(b * 4u + 4u), 0, 0);
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t rf = uniform_rsrc(
+      a.frame_off ? (const void *)a.frame_off : (const void *)a.offsets,
+      (live && a.frame_off) ? 0x7FFFFFF0u : 0u);
+  const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rf, (int)((f + (lane & 1u)) * 8u), 0, 0);
+  h.fo_lo = v.x;
+  h.fo_hi = v.y;
+  const __amdgpu_buffer_rsrc_t ri = uniform_rsrc(
+      a.block_init ? (const void *)(a.block_init + (uint64_t)f * a.nb) : (const void *)a.offsets,
+      (live && a.block_init) ? a.nb : 0u);
+  h.init = __builtin_amdgcn_raw_buffer_load_b8(ri, (int)b, 0, 0);
+}
+
+// Everything derived from a header once its loads have landed.
+struct Tile {
+  uint32_t tile, f, b0;
+  bool valid;          // this lane holds a block
+  uint32_t p;          // lane's start bit relative to the staged span
+  uint32_t start;      // span start byte (16-aligned, frame relative)
+  uint32_t span;       // span bytes (0xFFFFFFFF: unknown / corrupt)
+  uint32_t fb32;       // frame bytes (clamped to u32)
+  uint64_t fbeg;
+  uint32_t init;
+  uint32_t span_end_bits;  // end bit of the tile's last block (frame relative)
+};
+
+__device__ __forceinline__ Tile hdr_resolve(const DecodeArgs &a, const TileHdr &h, uint32_t lane) {
+  Tile t;
+  t.tile = h.tile;
+  t.f = h.tile / a.tiles_per_frame;
+  t.b0 = (h.tile - t.f * a.tiles_per_frame) * 64u;
+  const uint32_t b = t.b0 + lane;
+  t.valid = b < a.nb;
+  uint64_t fbytes = a.codes_bytes;
+  t.fbeg = 0;
+  if (a.frame_off) {
+    const uint64_t lo = ((uint64_t)__builtin_amdgcn_readlane(h.fo_hi, 0) << 32) |
+                        __builtin_amdgcn_readlane(h.fo_lo, 0);
+    const uint64_t hi = ((uint64_t)__builtin_amdgcn_readlane(h.fo_hi, 1) << 32) |
+                        __builtin_amdgcn_readlane(h.fo_lo, 1);
+    t.fbeg = lo;
+    fbytes = hi - lo;
+  }
+  t.fb32 = (uint32_t)(fbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : fbytes);
+  const uint32_t fbits = t.fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : t.fb32 * 8u;
+  const uint32_t end_l = (b + 1u < a.nb) ? h.nxt : fbits;
+  const uint32_t last = min(63u, a.nb - 1u - t.b0);  // last lane holding a block
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(h.off);
+  const uint32_t eb = __builtin_amdgcn_readlane(end_l, last);
+  t.span_end_bits = eb;
+  t.start = (sb >> 3) & ~15u;
+  uint32_t end = (eb >> 3) + 24u;
+  if (end > t.fb32 + 16u) end = t.fb32 + 16u;
+  t.span = end > t.start ? ((end - t.start + 15u) & ~15u) : 0xFFFFFFFFu;
+  t.p = t.valid ? h.off - t.start * 8u : 0u;
+  t.init = h.init & 0xFFu;
+  // materialise every header-derived value now: the loads are a tile old, and no
+  // later use may make the compiler wait on the span prefetch issued after this
+  asm volatile("" ::"v"(t.p), "v"(t.init));
+  return t;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t codes_rsrc(const DecodeArgs &a, const Tile &t) {
+  return uniform_rsrc(a.codes + t.fbeg, t.fb32);
+}
+
+__device__ __forceinline__ void span_issue(const DecodeArgs &a, const Tile &t, uint32_t lane,
+                                           v4u32 (&R)[kStageChunks]) {
+  // Unconditional loads (no exec-masked branches, so the compiler can count them
+  // in vmcnt); chunks past the span use an offset outside the descriptor's range,
+  // which returns 0 without a memory access.
+  const __amdgpu_buffer_rsrc_t rc = codes_rsrc(a, t);
+#pragma unroll
+  for (int k = 0; k < kStageChunks; ++k) {
+    const uint32_t c = lane + 64u * k;
+    const uint32_t off = c * 16u < t.span ? t.start + c * 16u : 0xFFFFFFF0u;
+    R[k] = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)off, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void span_write(const Tile &t, uint32_t lane, const v4u32 (&R)[kStageChunks],
+                                           uint8_t *stage) {
+#pragma unroll
+  for (int k = 0; k < kStageChunks; ++k) {
+    const uint32_t c = lane + 64u * k;
+    if (c * 16u < t.span) {
+      v4u32 v = R[k];
+      v.x = bswap32(v.x);
+      v.y = bswap32(v.y);
+      v.z = bswap32(v.z);
+      v.w = bswap32(v.w);
+      *reinterpret_cast<v4u32 *>(stage + c * 16u) = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Oversize tile: stage + decode lanes [0,32) then [32,64), each from its own span.
 template <bool kDelta>
-__global__ void __launch_bounds__(64 * kMaxWavesPerWG) mh_decode_kernel(const DecodeArgs a) {
+__device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t, uint32_t lane,
+                                                        uint8_t *stage, __amdgpu_buffer_rsrc_t out,
+                                                        uint32_t row0, bool dead) {
+  const __amdgpu_buffer_rsrc_t rc = codes_rsrc(a, t);
+  const uint32_t my_off = t.p + t.start * 8u;  // lane's absolute start bit
+  const uint32_t fbits = t.fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : t.fb32 * 8u;
+#pragma unroll 1
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t first = h * 32u;
+    const uint32_t sb = __builtin_amdgcn_readlane(my_off, first);
+    // end of the half: start bit of lane first+32 (or the tile's last block end)
+    const uint32_t nblk = a.nb - t.b0;  // blocks in this tile (may be < 64)
+    if (first >= nblk) break;
+    uint32_t eb;
+    if (first + 32u < nblk) {
+      eb = __builtin_amdgcn_readlane(my_off, first + 32u);
+    } else {
+      eb = t.span_end_bits;
+    }
+    const uint32_t start = (sb >> 3) & ~15u;
+    uint32_t end = (eb >> 3) + 24u;
+    if (end > t.fb32 + 16u) end = t.fb32 + 16u;
+    const uint32_t span = min((end - start + 15u) & ~15u, (uint32_t)kStageBytes);
+    __builtin_amdgcn_s_waitcnt(0);  // rare path: drain before reusing the window
+    for (uint32_t c = lane; c * 16u < span; c += 64u) {
+      v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(start + c * 16u), 0, 0);
+      v.x = bswap32(v.x);
+      v.y = bswap32(v.y);
+      v.z = bswap32(v.z);
+      v.w = bswap32(v.w);
+      *reinterpret_cast<v4u32 *>(stage + c * 16u) = v;
+    }
+    wave_sync();
+    if (lane >= first && lane < first + 32u) {
+      LdsWords src{reinterpret_cast<const uint32_t *>(stage)};
+      decode_block<kDelta>(src, t.valid ? my_off - start * 8u : 0u, t.init, out, row0,
+                           (uint32_t)a.out_pitch, dead);
+    }
+    wave_sync();
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  (void)fbits;
+}
+
+// Persistent loop: wave w of workgroup g decodes tiles g*W + w, + gridDim*W, ...
+// Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
+// header of tile i+2 and the code span of tile i+1 are in flight into registers;
+// the span is written to the wave's LDS window once tile i has finished reading it.
+template <bool kDelta>
+__global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_decode_kernel(const DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = blockDim.x >> 6;
+  const uint32_t gstride = gridDim.x * nwaves;
   uint8_t *stage = s_stage + wave * kStageBytes;
+
+  TileHdr hc, hn;
+  hdr_issue(a, blockIdx.x * nwaves + wave, lane, hc);
 
   // ---- lookup table into LDS (shared by the workgroup) ----
   if (a.lut) {
     const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
     for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
-    __syncthreads();
-  } else {
-    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x,
-              [] { __syncthreads(); });
   }
 
-  for (uint32_t g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
-    const uint32_t tile = g * nwaves + wave;
-    if (tile >= a.total_tiles) break;  // wave-uniform
-    const uint32_t f = tile / a.tiles_per_frame;
-    const uint32_t b0 = (tile - f * a.tiles_per_frame) * 64u;
-    const uint32_t b = b0 + lane;
-    const bool valid = b < a.nb;
+  v4u32 R[kStageChunks];
+  Tile cur;
+  cur.tile = hc.tile;
+  bool cur_staged = false;
+  if (hc.tile < a.total_tiles) {
+    cur = hdr_resolve(a, hc, lane);
+    cur_staged = cur.span <= (uint32_t)kStageBytes;
+    if (cur_staged) span_issue(a, cur, lane, R);
+  }
+  hdr_issue(a, hc.tile + gstride, lane, hn);
 
-    uint64_t fbeg = 0, fbytes = a.codes_bytes;
-    if (a.frame_off) {
-      fbeg = a.frame_off[f];
-      fbytes = a.frame_off[f + 1] - fbeg;
-    }
-    const uint32_t *offs = a.offsets + (uint64_t)f * a.nb;
-    const uint32_t off = valid ? offs[b] : 0u;
-    const uint32_t sb = __builtin_amdgcn_readfirstlane(off);  // lane 0 is always valid
-    const uint32_t fb32 = (uint32_t)(fbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : fbytes);
-    const uint32_t eb = (b0 + 64u < a.nb) ? offs[b0 + 64u] : (fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : fb32 * 8u);
-    const uint32_t start = (sb >> 3) & ~15u;
-    uint32_t end = (eb >> 3) + 24u;
-    if (end > fb32 + 16u) end = fb32 + 16u;
-    const uint32_t span = end > start ? ((end - start + 15u) & ~15u) : 0xFFFFFFFFu;
+  if (a.lut) {
+    __syncthreads();
+  } else {
+    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
+  }
+  if (cur.tile < a.total_tiles && cur_staged) span_write(cur, lane, R, stage);
+  Tile nxt;
+  nxt.tile = hn.tile;
+  if (hn.tile < a.total_tiles) nxt = hdr_resolve(a, hn, lane);
 
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.codes + fbeg), (short)0, (int)fb32, 0x00020000);
+  // Per iteration the only VMEM issued after a prefetch is the 8 unconditional row
+  // stores, so every wait below is an exact vmcnt that leaves the stores in flight.
+  while (cur.tile < a.total_tiles) {  // wave-uniform
+    if (__builtin_expect(!cur_staged, 0)) break;  // oversize span: finish in the slow loop
+    const bool nxt_live = nxt.tile < a.total_tiles;
+    const bool nxt_staged = nxt_live && nxt.span <= (uint32_t)kStageBytes;
+    if (nxt_staged) span_issue(a, nxt, lane, R);
+    hdr_issue(a, nxt.tile + gstride, lane, hn);
 
-    const uint32_t p = valid ? off - start * 8u : 0u;
-    const uint32_t prev = (valid && a.block_init) ? a.block_init[(uint64_t)f * a.nb + b] : 0u;
-    const uint32_t bx = b % a.bw, by = b / a.bw;
-    const uint32_t cols = min(8u, a.w - min(a.w, bx * 8u));
-    const uint32_t rows = min(8u, a.h - min(a.h, by * 8u));
-    uint8_t *dst = a.out + (uint64_t)f * a.out_frame_stride + (uint64_t)by * 8u * a.out_pitch + bx * 8u;
-
-    if (span <= (uint32_t)kStageBytes) {
-      for (uint32_t c = lane; c * 16u < span; c += 64u) {
-        v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(start + c * 16u), 0, 0);
-        v.x = bswap32(v.x);
-        v.y = bswap32(v.y);
-        v.z = bswap32(v.z);
-        v.w = bswap32(v.w);
-        *reinterpret_cast<v4u32 *>(stage + c * 16u) = v;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();  // this tile's staging writes -> reads
+    {
+      const uint32_t b = cur.b0 + lane;
+      const uint32_t bx = b % a.bw, by = b / a.bw;
+      const bool dead = !cur.valid;
+      const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
+      const __amdgpu_buffer_rsrc_t out =
+          uniform_rsrc(a.out + (uint64_t)cur.f * a.out_frame_stride, a.out_frame_bytes);
       LdsWords src{reinterpret_cast<const uint32_t *>(stage)};
-      decode_block<kDelta>(src, p, prev, valid, dst, a.out_pitch, cols, rows);
-      // the next tile's staging writes stay behind this tile's reads
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      GlobalWords src{rsrc, start};
-      decode_block<kDelta>(src, p, prev, valid, dst, a.out_pitch, cols, rows);
+      decode_block<kDelta>(src, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
     }
+    wave_sync();  // this tile's reads -> next tile's staging writes
+    if (nxt_staged) span_write(nxt, lane, R, stage);
+    Tile nn;
+    nn.tile = hn.tile;
+    if (nxt_live && hn.tile < a.total_tiles) nn = hdr_resolve(a, hn, lane);
+    cur = nxt;
+    cur_staged = nxt_staged;
+    nxt = nn;
+  }
+
+  // Slow loop (rare): a tile whose code span exceeds the LDS window (long codes in
+  // most of its 64 blocks) and every later tile of this wave, without prefetch.
+  // Kept after the pipelined loop so its waits never merge into that loop.
+  for (uint32_t t = cur.tile; t < a.total_tiles; t += gstride) {
+    __builtin_amdgcn_s_waitcnt(0);
+    TileHdr h;
+    hdr_issue(a, t, lane, h);
+    const Tile tt = hdr_resolve(a, h, lane);
+    const uint32_t b = tt.b0 + lane;
+    const uint32_t bx = b % a.bw, by = b / a.bw;
+    const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
+    const __amdgpu_buffer_rsrc_t out =
+        uniform_rsrc(a.out + (uint64_t)tt.f * a.out_frame_stride, a.out_frame_bytes);
+    decode_halves<kDelta>(a, tt, lane, stage, out, row0, !tt.valid);
   }
 }
 
@@ -389,6 +589,7 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (out_pitch < d.width || (fr->n_frames > 1 && out_frame_stride < out_pitch * d.height))
     return MH_ERR_CAPACITY;
   if (fr->codes_bytes < MH_CODES_PAD) return MH_ERR_CAPACITY;
+  if ((uint64_t)d.height * out_pitch > 0x7FFFFFF0ull) return MH_ERR_CAPACITY;  // store descriptor range
   if (fr->n_frames == 1 && !fr->d_frame_code_offsets && fr->codes_bytes > 0xFFFFFFF0ull)
     return MH_ERR_CAPACITY;
 
@@ -404,6 +605,7 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   a.out = d_out;
   a.out_pitch = out_pitch;
   a.out_frame_stride = out_frame_stride;
+  a.out_frame_bytes = (uint32_t)((uint64_t)d.height * out_pitch);
   a.t2_entries = fr->table2_entries;
   a.w = d.width;
   a.h = d.height;
