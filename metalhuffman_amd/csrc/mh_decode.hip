@@ -43,6 +43,12 @@ namespace {
 #ifndef MH_NT_STORE
 #define MH_NT_STORE 1
 #endif
+#ifndef MH_SPEC_REFILL          // 1: refill folded into the pair's first lookup (A/B)
+#define MH_SPEC_REFILL 0
+#endif
+#ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
+#define MH_DIAG_STAMPS 0
+#endif
 constexpr int kLutBits = 13;                  // first-level index width
 constexpr int kL1Entries = 1 << kLutBits;     // 8192 x u16
 constexpr int kL2Bits = 16 - kLutBits;        // 3 more window bits for long codes
@@ -54,6 +60,7 @@ constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile s
 constexpr int kMaxWavesPerWG = MH_MAX_WAVES;
 static_assert(kLutBytes % 16 == 0, "lut copy uses 16-byte chunks");
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
+static_assert(kL2Subtables < 240, "escape entries must stay below the smallest step word");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
@@ -92,15 +99,30 @@ __device__ __forceinline__ uint32_t split_lookup(const uint16_t *t1, const uint1
   return e;
 }
 
+// LUT entry format ("step word"): a valid {symbol, bitWidth} becomes
+//   E = (symbol << 8) - bitWidth  (mod 2^16),
+// so ONE add of E to the lane state S (see decode_block) advances the bit cursor
+// (low byte) and folds the delta into prev (byte 1). Valid entries have a low
+// byte in [240, 255] (bitWidth 1..16), so E >= 240. Escapes to the second level
+// are E = sub < 129, and a window the table does not decode ({0,0} in the
+// reference) is E = 0: adding it changes nothing, exactly the reference's
+// zero-width step.
+__device__ __forceinline__ uint32_t step_word(uint32_t e) {
+  const uint32_t len = e >> 8;
+  return len ? (((e & 0xFFu) << 8) - len) & 0xFFFFu : 0u;
+}
+constexpr uint32_t kEscapeBelow = 240u;
+
 // Builds the two-level table into `lut` (LDS or global) with `nthreads`
 // cooperating threads; `p0` is a scratch word shared by them.
-//   L1[p] (p = 13-bit prefix): split_lookup(p << 3) when that code has <= 13 bits
-//     or the window is invalid (entry 0 -> dummy subtable 0 -> {0,0}, as the
-//     reference's dummy T2 subtable, HuffmanUtil.cpp:550-556); otherwise an
-//     escape {sub, 0}. Canonical codes are ordered by length, so every code of
-//     14-16 bits lies at or above the first such code's prefix P0 and the long
-//     codes (<= 256 codes of >= 4 patterns) occupy at most 128 prefixes from P0.
-//   L2[sub*8 + x] = split_lookup(((P0 + sub - 1) << 3) | x), sub >= 1.
+//   L1[p] (p = 13-bit prefix): step_word(split_lookup(p << 3)) when that code has
+//     <= 13 bits or the window is invalid (0 -> no-op, as the reference's dummy
+//     T2 subtable, HuffmanUtil.cpp:550-556); otherwise an escape `sub`.
+//     Canonical codes are ordered by length, so every code of 14-16 bits lies at
+//     or above the first such code's prefix P0 and the long codes (<= 256 codes
+//     of >= 4 patterns) occupy at most 128 prefixes from P0.
+//   L2[sub*8 + x] = step_word(split_lookup(((P0 + sub - 1) << 3) | x)), sub >= 1;
+//   L2 subtable 0 is all zero (escapes beyond the long-code range: invalid windows).
 template <class SyncFn>
 __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_entries,
                           uint16_t *lut, uint32_t *p0, uint32_t tid, uint32_t nthreads,
@@ -109,7 +131,7 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
   sync();
   for (uint32_t p = tid; p < (uint32_t)kL1Entries; p += nthreads) {
     const uint32_t e = split_lookup(t1, t2, t2_entries, p << kL2Bits);
-    lut[p] = (uint16_t)e;
+    lut[p] = (uint16_t)step_word(e);
     if ((e >> 8) > (uint32_t)kLutBits) atomicMin(p0, p);
   }
   for (uint32_t i = tid; i < (uint32_t)(kLutEntries - kL1Entries); i += nthreads)
@@ -122,7 +144,8 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
   }
   const uint32_t nl2 = ((uint32_t)kL1Entries - P0) << kL2Bits;
   for (uint32_t i = tid; i < nl2 && i < (uint32_t)(kL2Entries - (1 << kL2Bits)); i += nthreads)
-    lut[kL1Entries + (1 << kL2Bits) + i] = (uint16_t)split_lookup(t1, t2, t2_entries, (P0 << kL2Bits) + i);
+    lut[kL1Entries + (1 << kL2Bits) + i] =
+        (uint16_t)step_word(split_lookup(t1, t2, t2_entries, (P0 << kL2Bits) + i));
   sync();
 }
 
@@ -132,63 +155,111 @@ __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1
   build_lut(t1, t2, t2_entries, lut, &p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
 }
 
-// Word sources for the bit cursor: big-endian dwords of the tile's code span.
+// Word source for the bit cursor: big-endian dwords of the tile's code span.
 struct LdsWords {
-  const uint32_t *w;
-  __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i]; }
+  const uint8_t *w;
+  __device__ __forceinline__ const uint8_t *at(uint32_t byte_off) const { return w + byte_off; }
 };
+__device__ __forceinline__ uint32_t word_at(const uint8_t *q) {
+  return *reinterpret_cast<const uint32_t *>(q);
+}
 
-// byte-insert selectors for v_perm_b32: put S0.byte0 at byte J, keep S1's others
-__device__ __forceinline__ constexpr uint32_t ins_sel(int j) {
-  return j == 0 ? 0x03020104u : j == 1 ? 0x03020400u : j == 2 ? 0x03040100u : 0x04020100u;
+// v_perm_b32 selectors: put S0.byte1 at byte J, keep S1's other bytes
+__device__ __forceinline__ constexpr uint32_t ins_sel1(int j) {
+  return j == 0 ? 0x03020105u : j == 1 ? 0x03020500u : j == 2 ? 0x03050100u : 0x05020100u;
 }
 
 __shared__ __attribute__((aligned(16))) uint16_t s_lut[kLutEntries];
 __shared__ __attribute__((aligned(16))) uint8_t s_stage[kMaxWavesPerWG * kStageBytes];
 __shared__ uint32_t s_p0;
 
+#if MH_DIAG_STAMPS
+constexpr int kDiagWaves = 8192, kDiagSlots = 8;
+__device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
+#define MH_STAMP(i) (ts[i] = __builtin_amdgcn_s_memrealtime())
+#else
+#define MH_STAMP(i) ((void)0)
+#endif
+
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
+//
+// Lane state: a 64-bit window hi:lo of big-endian code words, the LDS address
+// `wa` of hi in the staged span, the prefetched next word `nw`, and
+//   S: bits 0-7 = 114 - sh (sh = bits of hi:lo already consumed, 0..63),
+//      bits 8-15 = prev (the running delta sum), bits 16+ = don't care.
+// (hi:lo) >> (S & 63) = (hi:lo) >> (50 - sh) puts the next 13 code bits at bits
+// 1..13, i.e. the byte address of their u16 table entry; one add of the entry's
+// step word then advances sh and prev together (the low byte stays in [51, 114],
+// so it never borrows from prev).
 template <bool kDelta, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_t prev,
                                              __amdgpu_buffer_rsrc_t out, uint32_t row0,
                                              uint32_t pitch, bool dead) {
-  uint32_t wi = p >> 5;
-  uint32_t sh = p & 31u;
-  uint32_t hi = src(wi);
-  uint32_t lo = src(wi + 1);
-  wi += 2;
-  uint32_t nw = src(wi);
+  const uint8_t *wa = src.at((p >> 5) * 4u);
+  uint32_t S = (prev << 8) + 114u - (p & 31u);
+  uint32_t hi = word_at(wa);
+  uint32_t lo = word_at(wa + 4);
+  uint32_t nw = word_at(wa + 8);
+  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
 
-  // window = next 32 bits of the block's stream; sh <= 47 keeps >= 16 valid.
-#define MH_STEP(J, OW)                                                              \
+  // sh <= 47 at every lookup keeps >= 16 valid window bits.
+#define MH_LOOKUP(A1)                                                               \
+  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? 0u : (A1)));
+#define MH_FINISH(J, OW)                                                            \
   {                                                                                 \
-    const uint32_t win = (uint32_t)(((((uint64_t)hi) << 32) | lo) << sh >> 32);     \
-    uint32_t e = s_lut[MH_DIAG_BROADCAST_LUT ? 0u : (win >> (32 - kLutBits))];     \
-    const bool esc = e < 256u;                                                      \
+    const bool esc = e < kEscapeBelow;                                              \
     if (__builtin_expect(__ballot(esc) != 0, 0)) {                                  \
-      const uint32_t e2 = s_lut[kL1Entries + ((e & 0xFFu) << kL2Bits) +             \
-                                ((win >> (32 - 16)) & ((1u << kL2Bits) - 1u))];     \
+      const uint64_t x = (((uint64_t)hi) << 32) | lo;                               \
+      const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;                   \
+      const uint32_t e2 = s_lut[kL1Entries + ((e & 0xFFu) << kL2Bits) + x3];        \
       e = esc ? e2 : e;                                                             \
     }                                                                               \
-    sh += e >> 8;                                                                   \
+    S += e;                                                                         \
     if (kDelta) {                                                                   \
-      prev += e;                                                                    \
-      OW = __builtin_amdgcn_perm(prev, OW, ins_sel(J));                             \
+      OW = __builtin_amdgcn_perm(S, OW, ins_sel1(J));                               \
     } else {                                                                        \
-      OW = __builtin_amdgcn_perm(e, OW, ins_sel(J));                                \
+      OW = __builtin_amdgcn_perm(e + 0x100u, OW, ins_sel1(J));                      \
     }                                                                               \
   }
-  // keep sh < 32 at the start of every symbol pair (each code is <= 16 bits)
-#define MH_REFILL()                                                                 \
+  // sh <= 47 at every lookup keeps >= 16 valid window bits.
+#define MH_STEP(J, OW)                                                              \
   {                                                                                 \
-    const bool c = sh >= 32u;                                                       \
+    const uint64_t x = (((uint64_t)hi) << 32) | lo;                                 \
+    MH_LOOKUP((uint32_t)(x >> (S & 63u)) & 0x3FFEu)                                 \
+    MH_FINISH(J, OW)                                                                \
+  }
+  // keep sh < 32 at the start of every symbol pair (each code is <= 16 bits)
+#define MH_REFILL_C(c)                                                              \
+  {                                                                                 \
     hi = c ? lo : hi;                                                               \
     lo = c ? nw : lo;                                                               \
-    sh &= 31u;                                                                      \
-    wi += c ? 1u : 0u;                                                              \
-    nw = src(wi);                                                                   \
+    const uint32_t d = c ? 4u : 0u;                                                 \
+    wa += d;                                                                        \
+    S += d * 8u;                                                                    \
+    nw = word_at(wa + 8);                                                           \
   }
+#if MH_SPEC_REFILL
+  // First symbol of a pair with the refill folded in: the table address is taken
+  // from whichever window the refill will select (both shifts run in parallel),
+  // so the word move itself overlaps the LDS read instead of preceding it.
+#define MH_STEP_R(J, OW)                                                            \
+  {                                                                                 \
+    const bool c = (S & 0xFFu) <= 82u;                                              \
+    const uint32_t v0 = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (S & 63u));    \
+    const uint32_t v1 = (uint32_t)(((((uint64_t)lo) << 32) | nw) >> ((S + 32u) & 63u)); \
+    MH_LOOKUP((c ? v1 : v0) & 0x3FFEu)                                              \
+    MH_REFILL_C(c)                                                                  \
+    MH_FINISH(J, OW)                                                                \
+  }
+#else
+#define MH_STEP_R(J, OW)                                                            \
+  {                                                                                 \
+    const bool c = (S & 0xFFu) <= 82u;                                              \
+    MH_REFILL_C(c)                                                                  \
+    MH_STEP(J, OW)                                                                  \
+  }
+#endif
 
 #if MH_ROW_UNROLL == 8
 #pragma unroll
@@ -197,17 +268,17 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
 #endif
   for (uint32_t r = 0; r < 8; ++r) {
     uint32_t o0 = 0, o1 = 0;
-    if (r) MH_REFILL();
-    MH_STEP(0, o0);
+    if (r) {
+      MH_STEP_R(0, o0);
+    } else {
+      MH_STEP(0, o0);
+    }
     MH_STEP(1, o0);
-    MH_REFILL();
-    MH_STEP(2, o0);
+    MH_STEP_R(2, o0);
     MH_STEP(3, o0);
-    MH_REFILL();
-    MH_STEP(0, o1);
+    MH_STEP_R(0, o1);
     MH_STEP(1, o1);
-    MH_REFILL();
-    MH_STEP(2, o1);
+    MH_STEP_R(2, o1);
     MH_STEP(3, o1);
     // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
     // block and rows below the frame use offsets outside the descriptor's range,
@@ -223,7 +294,10 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
     }
   }
 #undef MH_STEP
-#undef MH_REFILL
+#undef MH_STEP_R
+#undef MH_LOOKUP
+#undef MH_FINISH
+#undef MH_REFILL_C
 }
 
 constexpr int kStageChunks = (kStageBytes / 16 + 63) / 64;  // 16-B chunks per lane (5)
@@ -400,7 +474,7 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
     }
     wave_sync();
     if (lane >= first && lane < first + 32u) {
-      LdsWords src{reinterpret_cast<const uint32_t *>(stage)};
+      LdsWords src{stage};
       decode_block<kDelta>(src, t.valid ? my_off - start * 8u : 0u, t.init, out, row0,
                            (uint32_t)a.out_pitch, dead);
     }
@@ -421,6 +495,11 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   const uint32_t nwaves = blockDim.x >> 6;
   const uint32_t gstride = gridDim.x * nwaves;
   uint8_t *stage = s_stage + wave * kStageBytes;
+#if MH_DIAG_STAMPS
+  unsigned long long ts[kDiagSlots] = {};
+  bool first_tile = true;
+#endif
+  MH_STAMP(0);
 
   TileHdr hc, hn;
   hdr_issue(a, blockIdx.x * nwaves + wave, lane, hc);
@@ -438,6 +517,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   bool cur_staged = false;
   if (hc.tile < a.total_tiles) {
     cur = hdr_resolve(a, hc, lane);
+    MH_STAMP(1);
     cur_staged = cur.span <= (uint32_t)kStageBytes;
     if (cur_staged) span_issue(a, cur, lane, R);
   }
@@ -448,7 +528,9 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   } else {
     build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
+  MH_STAMP(2);
   if (cur.tile < a.total_tiles && cur_staged) span_write(cur, lane, R, stage);
+  MH_STAMP(3);
   Tile nxt;
   nxt.tile = hn.tile;
   if (hn.tile < a.total_tiles) nxt = hdr_resolve(a, hn, lane);
@@ -470,9 +552,13 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
       const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
       const __amdgpu_buffer_rsrc_t out =
           uniform_rsrc(a.out + (uint64_t)cur.f * a.out_frame_stride, a.out_frame_bytes);
-      LdsWords src{reinterpret_cast<const uint32_t *>(stage)};
+      LdsWords src{stage};
       decode_block<kDelta>(src, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
     }
+#if MH_DIAG_STAMPS
+    if (first_tile) MH_STAMP(4);
+    first_tile = false;
+#endif
     wave_sync();  // this tile's reads -> next tile's staging writes
     if (nxt_staged) span_write(nxt, lane, R, stage);
     Tile nn;
@@ -498,6 +584,16 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
         uniform_rsrc(a.out + (uint64_t)tt.f * a.out_frame_stride, a.out_frame_bytes);
     decode_halves<kDelta>(a, tt, lane, stage, out, row0, !tt.valid);
   }
+#if MH_DIAG_STAMPS
+  MH_STAMP(5);
+  __builtin_amdgcn_s_waitcnt(0);
+  MH_STAMP(6);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+  ts[7] = ((unsigned long long)xcc << 48) | ((unsigned long long)__smid() << 32) | blockIdx.x;
+  const uint32_t gw = blockIdx.x * nwaves + wave;
+  if (lane == 0 && gw < (uint32_t)kDiagWaves)
+    for (int i = 0; i < kDiagSlots; ++i) g_stamps[gw * kDiagSlots + i] = ts[i];
+#endif
 }
 
 int g_cu_count = 0;
@@ -548,6 +644,14 @@ int launch(const DecodeArgs &a0, hipStream_t s) {
 }  // namespace
 
 extern "C" {
+
+#if MH_DIAG_STAMPS
+int mh_diag_stamps(unsigned long long *host, size_t n) {
+  if (n > sizeof(g_stamps) / sizeof(g_stamps[0])) n = sizeof(g_stamps) / sizeof(g_stamps[0]);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+#endif
 
 size_t mh_lut_bytes(void) { return (size_t)kLutBytes; }
 int mh_lut_bits(void) { return kLutBits; }

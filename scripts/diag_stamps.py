@@ -1,0 +1,62 @@
+"""Phase timeline of one decode launch from a MH_DIAG_STAMPS=1 build (GPU, diagnostic).
+
+    MH_LIB=metalhuffman_amd/_variants/lib_diag.so python scripts/diag_stamps.py [--batch N]
+
+Stamps (s_memrealtime, 100 MHz) per wave: 0 entry, 1 first header resolved,
+2 LUT ready, 3 first span staged, 4 first tile decoded (stores issued),
+5 loop done, 6 stores drained.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import metalhuffman_amd as mh  # noqa: E402
+from metalhuffman_amd import _native as N, decoder as D, frames as F  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--reps", type=int, default=20)
+args = ap.parse_args()
+
+lib = N.lib()
+if not hasattr(lib, "mh_diag_stamps"):
+    sys.exit("not a MH_DIAG_STAMPS build (set MH_LIB)")
+bb = F.bigbridge()
+efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.batch)]
+t1, t2 = efs[0].tables()
+tabs = D.DeviceTables.upload(t1, t2, "cuda")
+fr = D.DeviceFrames.pack(efs, "cuda")
+out = D.decode(fr, tabs)
+for _ in range(args.reps):
+    D.decode(fr, tabs, out)
+torch.cuda.synchronize()
+s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s0.record()
+D.decode(fr, tabs, out)
+s1.record()
+torch.cuda.synchronize()
+n = 8192 * 8
+buf = (ctypes.c_ulonglong * n)()
+assert lib.mh_diag_stamps(buf, ctypes.c_size_t(n)) == n
+st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)
+live = st[:, 0] > 0
+st = st[live]
+t0 = st[:, 0].min()
+print(f"launch event time {s0.elapsed_time(s1) * 1e3:.2f} us; waves {live.sum()}")
+names = ["entry", "hdr", "lut", "staged", "tile0", "loop", "drain"]
+for i, nm in enumerate(names):
+    v = (st[:, i].astype(np.int64) - int(t0)) * 0.01
+    print(f"{nm:7s} us  min {v.min():7.2f}  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}  max {v.max():7.2f}")
+for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6)]:
+    d = (st[:, b].astype(np.int64) - st[:, a].astype(np.int64)) * 0.01
+    print(f"{names[a]}->{names[b]:7s} p50 {np.median(d):7.2f}  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f}")
+out_npz = os.path.join(ROOT, "gpurun_out", f"stamps_b{args.batch}.npz")
+os.makedirs(os.path.dirname(out_npz), exist_ok=True)
+np.savez(out_npz, stamps=np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8))
