@@ -236,14 +236,17 @@ def main(argv=None) -> int:
     for ef in efs:
         assert np.array_equal(ef.canon, efs[0].canon)
 
+    def pack(group):
+        return D.DeviceFrames.pack(group, dev)
+
     def frame_workload():
-        launches = [D.DeviceFrames.pack([ef], dev) for ef in efs]
+        launches = [pack([ef]) for ef in efs]
         return Workload("frame", launches, tables, bb.size, algo_bytes(efs[:1], t2_bytes), dev)
 
     def batch_workload(nb):
         groups = [efs[i:i + nb] for i in range(0, len(efs), nb)]
         groups = [g for g in groups if len(g) == nb] or [efs[:nb]]
-        launches = [D.DeviceFrames.pack(g, dev) for g in groups]
+        launches = [pack(g) for g in groups]
         return Workload(f"batch{nb}", launches, tables, nb * bb.size, algo_bytes(groups[0], t2_bytes), dev)
 
     def tile_workload():
@@ -252,7 +255,7 @@ def main(argv=None) -> int:
         tefs = encode_many(imgs, threads=3)
         t1t, t2t = tefs[0].tables()
         ttabs = D.DeviceTables.upload(t1t, t2t, dev)
-        launches = [D.DeviceFrames.pack([ef], dev) for ef in tefs]
+        launches = [pack([ef]) for ef in tefs]
         return Workload("tile8192", launches, ttabs, base.size, algo_bytes(tefs[:1], ttabs.table2.numel()), dev)
 
     if args.workload == "frame":

@@ -46,6 +46,9 @@ namespace {
 #ifndef MH_SPEC_REFILL          // 1: refill folded into the pair's first lookup (A/B)
 #define MH_SPEC_REFILL 0
 #endif
+#ifndef MH_PRIO_ROTATE          // wave priority: 0 off, 1 rotate per tile, 2 per block row,
+#define MH_PRIO_ROTATE 3        // 3 by remaining tiles (default)
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -181,6 +184,18 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 #define MH_STAMP(i) ((void)0)
 #endif
 
+// Wave priority 0..3 (s_setprio takes an immediate). The SIMD arbiter serves the
+// oldest wave first among equal priorities, so waves of later workgroups fall
+// behind; rotating every wave through all four levels evens out their progress.
+[[maybe_unused]] __device__ __forceinline__ void set_prio(uint32_t p) {
+  switch (__builtin_amdgcn_readfirstlane(p) & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
 //
@@ -195,7 +210,7 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 template <bool kDelta, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_t prev,
                                              __amdgpu_buffer_rsrc_t out, uint32_t row0,
-                                             uint32_t pitch, bool dead) {
+                                             uint32_t pitch, bool dead, uint32_t prio = 0) {
   const uint8_t *wa = src.at((p >> 5) * 4u);
   uint32_t S = (prev << 8) + 114u - (p & 31u);
   uint32_t hi = word_at(wa);
@@ -267,6 +282,9 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
 #pragma unroll 1
 #endif
   for (uint32_t r = 0; r < 8; ++r) {
+#if MH_PRIO_ROTATE == 2
+    set_prio(prio + r);
+#endif
     uint32_t o0 = 0, o1 = 0;
     if (r) {
       MH_STEP_R(0, o0);
@@ -403,15 +421,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t codes_rsrc(const DecodeArgs &a
 }
 
 __device__ __forceinline__ void span_issue(const DecodeArgs &a, const Tile &t, uint32_t lane,
-                                           v4u32 (&R)[kStageChunks]) {
+                                           v4u32 (&R)[kStageChunks], bool on = true) {
   // Unconditional loads (no exec-masked branches, so the compiler can count them
   // in vmcnt); chunks past the span use an offset outside the descriptor's range,
   // which returns 0 without a memory access.
-  const __amdgpu_buffer_rsrc_t rc = codes_rsrc(a, t);
+  // not `on`: a zero-record descriptor, so no offset can reach memory
+  const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(a.codes + (on ? t.fbeg : 0ull), on ? t.fb32 : 0u);
+  // one wave-uniform byte count, so the compiler cannot split the loads by `on`
+  const uint32_t span = __builtin_amdgcn_readfirstlane(on ? t.span : 0u);
 #pragma unroll
   for (int k = 0; k < kStageChunks; ++k) {
     const uint32_t c = lane + 64u * k;
-    const uint32_t off = c * 16u < t.span ? t.start + c * 16u : 0xFFFFFFF0u;
+    const uint32_t off = c * 16u < span ? t.start + c * 16u : 0xFFFFFFF0u;
     R[k] = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)off, 0, 0);
   }
 }
@@ -501,8 +522,12 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 #endif
   MH_STAMP(0);
 
+  uint32_t prio = blockIdx.x * nwaves + wave;  // rotation phase (MH_PRIO_ROTATE 1, 2)
+  // static grid-stride schedule; a tile id >= total_tiles means "no tile"
+  const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
+  const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
-  hdr_issue(a, blockIdx.x * nwaves + wave, lane, hc);
+  hdr_issue(a, t0, lane, hc);
 
   // ---- lookup table into LDS (shared by the workgroup) ----
   if (a.lut) {
@@ -512,16 +537,11 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   }
 
   v4u32 R[kStageChunks];
-  Tile cur;
-  cur.tile = hc.tile;
-  bool cur_staged = false;
-  if (hc.tile < a.total_tiles) {
-    cur = hdr_resolve(a, hc, lane);
-    MH_STAMP(1);
-    cur_staged = cur.span <= (uint32_t)kStageBytes;
-    if (cur_staged) span_issue(a, cur, lane, R);
-  }
-  hdr_issue(a, hc.tile + gstride, lane, hn);
+  Tile cur = hdr_resolve(a, hc, lane);
+  MH_STAMP(1);
+  bool cur_staged = cur.tile < a.total_tiles && cur.span <= (uint32_t)kStageBytes;
+  span_issue(a, cur, lane, R, cur_staged);
+  hdr_issue(a, next_tile(t0), lane, hn);
 
   if (a.lut) {
     __syncthreads();
@@ -529,11 +549,11 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
   MH_STAMP(2);
-  if (cur.tile < a.total_tiles && cur_staged) span_write(cur, lane, R, stage);
+  if (cur_staged) span_write(cur, lane, R, stage);
   MH_STAMP(3);
-  Tile nxt;
-  nxt.tile = hn.tile;
-  if (hn.tile < a.total_tiles) nxt = hdr_resolve(a, hn, lane);
+  // Resolved even past the end (zero-record loads): every Tile field is defined
+  // before span_issue builds a descriptor from it.
+  Tile nxt = hdr_resolve(a, hn, lane);
 
   // Per iteration the only VMEM issued after a prefetch is the 8 unconditional row
   // stores, so every wait below is an exact vmcnt that leaves the stores in flight.
@@ -541,8 +561,8 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     if (__builtin_expect(!cur_staged, 0)) break;  // oversize span: finish in the slow loop
     const bool nxt_live = nxt.tile < a.total_tiles;
     const bool nxt_staged = nxt_live && nxt.span <= (uint32_t)kStageBytes;
-    if (nxt_staged) span_issue(a, nxt, lane, R);
-    hdr_issue(a, nxt.tile + gstride, lane, hn);
+    span_issue(a, nxt, lane, R, nxt_staged);  // unconditional (all out of range if not staged)
+    hdr_issue(a, next_tile(nxt.tile), lane, hn);
 
     wave_sync();  // this tile's staging writes -> reads
     {
@@ -553,7 +573,14 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
       const __amdgpu_buffer_rsrc_t out =
           uniform_rsrc(a.out + (uint64_t)cur.f * a.out_frame_stride, a.out_frame_bytes);
       LdsWords src{stage};
-      decode_block<kDelta>(src, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
+#if MH_PRIO_ROTATE == 1
+      set_prio(prio);
+#elif MH_PRIO_ROTATE == 3
+      // waves with more tiles left run first (the arbiter otherwise favours the oldest)
+      set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
+#endif
+      decode_block<kDelta>(src, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead, prio);
+      prio += MH_PRIO_ROTATE == 2 ? 3u : 1u;
     }
 #if MH_DIAG_STAMPS
     if (first_tile) MH_STAMP(4);
@@ -561,9 +588,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 #endif
     wave_sync();  // this tile's reads -> next tile's staging writes
     if (nxt_staged) span_write(nxt, lane, R, stage);
-    Tile nn;
-    nn.tile = hn.tile;
-    if (nxt_live && hn.tile < a.total_tiles) nn = hdr_resolve(a, hn, lane);
+    const Tile nn = hdr_resolve(a, hn, lane);
     cur = nxt;
     cur_staged = nxt_staged;
     nxt = nn;
@@ -572,7 +597,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   // Slow loop (rare): a tile whose code span exceeds the LDS window (long codes in
   // most of its 64 blocks) and every later tile of this wave, without prefetch.
   // Kept after the pipelined loop so its waits never merge into that loop.
-  for (uint32_t t = cur.tile; t < a.total_tiles; t += gstride) {
+  for (uint32_t t = cur.tile; t < a.total_tiles; t = next_tile(t)) {
     __builtin_amdgcn_s_waitcnt(0);
     TileHdr h;
     hdr_issue(a, t, lane, h);

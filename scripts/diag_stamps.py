@@ -23,6 +23,7 @@ from metalhuffman_amd import _native as N, decoder as D, frames as F  # noqa: E4
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--tag", default="")
 args = ap.parse_args()
 
 lib = N.lib()
@@ -57,6 +58,6 @@ for i, nm in enumerate(names):
 for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6)]:
     d = (st[:, b].astype(np.int64) - st[:, a].astype(np.int64)) * 0.01
     print(f"{names[a]}->{names[b]:7s} p50 {np.median(d):7.2f}  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f}")
-out_npz = os.path.join(ROOT, "gpurun_out", f"stamps_b{args.batch}.npz")
+out_npz = os.path.join(ROOT, "gpurun_out", f"stamps_b{args.batch}{args.tag}.npz")
 os.makedirs(os.path.dirname(out_npz), exist_ok=True)
 np.savez(out_npz, stamps=np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8))

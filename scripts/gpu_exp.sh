@@ -1,4 +1,4 @@
-# Experiment round: parity on the default library, A/B of variants, diag timeline.
+# Experiment round: parity on the default library, A/B of variants, diag timelines.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -7,9 +7,14 @@ rc=$?
 tail -3 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/pytest_gpu.log | head -20; exit 1; }
 STEPS=${STEPS:-400} bash scripts/gpu_ab.sh || exit 1
-if [ -f metalhuffman_amd/_variants/lib_diag.so ]; then
-  export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_diag.so
-  timeout -k 10 300 python scripts/diag_stamps.py --batch 1 > gpurun_out/diag1.txt 2>&1 || exit 1
-  timeout -k 10 300 python scripts/diag_stamps.py --batch 64 > gpurun_out/diag64.txt 2>&1 || exit 1
-  cat gpurun_out/diag1.txt gpurun_out/diag64.txt
+for d in ${DIAGS:-diag}; do
+  [ -f metalhuffman_amd/_variants/lib_$d.so ] || continue
+  export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$d.so
+  timeout -k 10 300 python scripts/diag_stamps.py --batch 64 ${DIAG_ARGS:-} --tag _$d > gpurun_out/diag64_$d.txt 2>&1 || exit 1
+  echo "== $d"; tail -7 gpurun_out/diag64_$d.txt
+done
+if [ -n "${PROF_FRAME:-}" ]; then
+  unset MH_LIB
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/ktrace -o kt -- python3 bench.py --workload frame --steps 200 --warmup 20 --no-extras --no-cpu-baseline > gpurun_out/ktrace.log 2>&1 || exit 1
 fi

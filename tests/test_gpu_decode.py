@@ -86,6 +86,41 @@ def test_batch_block_shuffled(mh, device, bigbridge):
         assert np.array_equal(out[i], im), i
 
 
+def _decode_repeat(efs, device, reps):
+    import torch
+    from metalhuffman_amd import decoder as D
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    fr = D.DeviceFrames.pack(efs, device)
+    outs = []
+    for _ in range(reps):
+        out = D.decode(fr, tabs)
+        torch.cuda.synchronize(device)
+        outs.append(out[..., : fr.width].cpu().numpy())
+    return outs
+
+
+def test_multi_tile_waves_repeat(mh, device, bigbridge):
+    """Several tiles per wave (the pipelined loop's steady state), launched repeatedly
+    on the same buffers: every launch decodes every tile exactly once."""
+    from metalhuffman_amd import frames as F
+    imgs = [F.block_shuffle(bigbridge, 100 + s) for s in range(24)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    for out in _decode_repeat(efs, device, 3):
+        for i, im in enumerate(imgs):
+            assert np.array_equal(out[i], im), i
+
+
+def test_oversize_tiles_in_multi_tile_waves(mh, oracle, device):
+    """Tiles leave the pipelined loop for the slow path while waves hold several tiles."""
+    d = long_span_deltas(1024, 256)
+    img = image_from_block_deltas(d, 1024, 256)
+    ef = mh.encode_frame(img)
+    for out in _decode_repeat([ef] * 200, device, 2):  # 12,800 tiles
+        for i in range(200):
+            assert np.array_equal(out[i], img), i
+
+
 @pytest.mark.parametrize("n_sym", [14, 15, 17])
 def test_long_codes_delta(mh, oracle, device, n_sym):
     """Fibonacci histograms: codes up to 16 bits, exercising the second LDS level."""
