@@ -146,11 +146,27 @@ class Workload:
         return wall, region_ms, kms
 
 
-def roofline(bytes_per_launch, kernel_ms):
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def measured_traffic(workload: str):
+    """HBM bytes per launch of this workload from the committed PMC profile
+    (scripts/gpu_traffic.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH x2 on
+    gfx950), or None when no profile covers it."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            rec = json.load(f)["per_launch_median"].get(workload)
+        return int(rec["traffic_bytes"]) if rec else None
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def roofline(bytes_per_launch, kernel_ms, workload=None):
     avg_s = float(np.mean(kernel_ms)) * 1e-3
     ach = bytes_per_launch / avg_s / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": measured_traffic(workload) if workload else None,
             "kernel_us_avg": round(avg_s * 1e6, 3), "kernel_us_median": round(float(np.median(kernel_ms)) * 1e3, 3),
             "algorithmic_bytes_per_launch": int(bytes_per_launch)}
 
@@ -290,7 +306,7 @@ def main(argv=None) -> int:
                    "frames_per_step_per_gpu": int(wl.launches[0].n_frames),
                    "parallelism": f"frame-sharded x{world}", "launch": "hipGraph" if not args.no_graph else "eager"},
         "mpixels_per_s": round(value, 1),
-        "roofline": roofline(wl.bytes, kms),
+        "roofline": roofline(wl.bytes, kms, args.workload),
         "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
     }
     if t_bcast_us is not None:
@@ -298,8 +314,8 @@ def main(argv=None) -> int:
 
     if world == 1 and rank == 0 and not args.no_extras:
         extras = {}
-        for name, make, steps in (("batch64", lambda: batch_workload(args.batch), 20),
-                                  ("tile8192", tile_workload, 20)):
+        for name, make, steps, key in (("batch64", lambda: batch_workload(args.batch), 20, "batch"),
+                                       ("tile8192", tile_workload, 20, "tile8192")):
             if name.startswith("batch") and args.workload == "batch":
                 continue
             if name == "tile8192" and args.workload == "tile8192":
@@ -309,7 +325,7 @@ def main(argv=None) -> int:
             extras[name] = {"value_MBps": round(w2.pixels / (wall2 / steps) / 1e6, 1),
                             "ms_per_step": round(wall2 / steps * 1e3, 4),
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
-                            "roofline": roofline(w2.bytes, kms2)}
+                            "roofline": roofline(w2.bytes, kms2, key)}
             del w2
         result["extras"] = extras
 
