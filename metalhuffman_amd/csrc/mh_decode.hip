@@ -49,6 +49,9 @@ namespace {
 #ifndef MH_PRIO_ROTATE          // wave priority: 0 off, 1 rotate per tile, 2 per block row,
 #define MH_PRIO_ROTATE 3        // 3 by remaining tiles (default)
 #endif
+#ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
+#define MH_SMALL_KERNEL 1
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -58,10 +61,19 @@ constexpr int kL2Bits = 16 - kLutBits;        // 3 more window bits for long cod
 constexpr int kL2Subtables = 129;             // dummy + <=128 long-code prefixes
 constexpr int kL2Entries = kL2Subtables << kL2Bits;      // 1032
 constexpr int kLutEntries = kL1Entries + 1040;           // L1 + L2, padded to 16 B
-constexpr int kLutBytes = kLutEntries * 2;               // 18464
+constexpr int kLutBytes = kLutEntries * 2;               // 18464: the 13-bit table
+// The prepared table buffer (mh_prepare_lut) also holds a single-level 14-bit
+// table (no escapes; valid when no code exceeds 14 bits) and the longest code
+// length, for the small-launch kernel.
+constexpr int kLut14Bits = 14;
+constexpr int kLut14Entries = 1 << kLut14Bits;           // 16384 x u16
+constexpr int kLut14Off = kLutBytes;                     // byte offset in the buffer
+constexpr int kLut14Bytes = kLut14Entries * 2;           // 32768
+constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest code length
+constexpr int kPreparedBytes = kMaxLenOff + 16;          // 51248
 constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile span)
 constexpr int kMaxWavesPerWG = MH_MAX_WAVES;
-static_assert(kLutBytes % 16 == 0, "lut copy uses 16-byte chunks");
+static_assert(kLutBytes % 16 == 0 && kLut14Bytes % 16 == 0, "lut copy uses 16-byte chunks");
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
 static_assert(kL2Subtables < 240, "escape entries must stay below the smallest step word");
 
@@ -152,10 +164,30 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
   sync();
 }
 
+// Single-level 14-bit table: step_word of every window whose code has <= 14 bits
+// (0 otherwise), and the longest code length of the table into *max_len.
+__device__ void build_lut14(const uint16_t *t1, const uint16_t *t2, uint32_t t2_entries,
+                            uint16_t *lut14, uint32_t *max_len, uint32_t tid, uint32_t nthreads) {
+  uint32_t mx = 0;
+  for (uint32_t p = tid; p < (uint32_t)kLut14Entries; p += nthreads) {
+    const uint32_t e = split_lookup(t1, t2, t2_entries, p << (16 - kLut14Bits));
+    const uint32_t len = e >> 8;
+    lut14[p] = (uint16_t)(len <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
+    mx = max(mx, len);
+  }
+  atomicMax(max_len, mx);
+}
+
 __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1, const uint16_t *t2,
-                                                              uint32_t t2_entries, uint16_t *lut) {
-  __shared__ uint32_t p0;
-  build_lut(t1, t2, t2_entries, lut, &p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
+                                                              uint32_t t2_entries, uint8_t *buf) {
+  __shared__ uint32_t p0, mx;
+  if (threadIdx.x == 0) mx = 0;
+  build_lut(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf), &p0, threadIdx.x, blockDim.x,
+            [] { __syncthreads(); });
+  build_lut14(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf + kLut14Off), &mx, threadIdx.x,
+              blockDim.x);
+  __syncthreads();
+  if (threadIdx.x < 4) reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[threadIdx.x] = threadIdx.x ? 0u : mx;
 }
 
 // Word source for the bit cursor: big-endian dwords of the tile's code span.
@@ -196,39 +228,61 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
   }
 }
 
+// Lookup flavours of the decode step.
+//   Lut13: 2^13-entry first level + escapes to the second level (any code <= 16 bits).
+//   Lut14: 2^14-entry single level, no escape test at all; valid when no code is
+//          longer than 14 bits (the prepared table records the longest code).
+// kSpec: the table address of a pair's first symbol is taken from whichever
+//   window the refill selects (two shifts in parallel), taking the word move off
+//   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
+template <int kBits, bool kSpecRefill>
+struct StepCfg {
+  static constexpr bool kEsc = kBits == kLutBits;
+  static constexpr bool kSpec = kSpecRefill;
+  static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
+  static constexpr uint32_t kMask = (2u << kBits) - 2u;       // byte address of a u16 entry
+  static constexpr uint32_t kRefillAt = kCur - 32u;           // low byte <= this: sh >= 32
+};
+
+using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0>;  // the batch kernel's step
+
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
 //
 // Lane state: a 64-bit window hi:lo of big-endian code words, the LDS address
 // `wa` of hi in the staged span, the prefetched next word `nw`, and
-//   S: bits 0-7 = 114 - sh (sh = bits of hi:lo already consumed, 0..63),
+//   S: bits 0-7 = kCur - sh (sh = bits of hi:lo already consumed, 0..63),
 //      bits 8-15 = prev (the running delta sum), bits 16+ = don't care.
-// (hi:lo) >> (S & 63) = (hi:lo) >> (50 - sh) puts the next 13 code bits at bits
-// 1..13, i.e. the byte address of their u16 table entry; one add of the entry's
-// step word then advances sh and prev together (the low byte stays in [51, 114],
-// so it never borrows from prev).
-template <bool kDelta, class Src>
-__device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_t prev,
-                                             __amdgpu_buffer_rsrc_t out, uint32_t row0,
-                                             uint32_t pitch, bool dead, uint32_t prio = 0) {
+// (hi:lo) >> (S & 63) = (hi:lo) >> (kCur - 64 - sh) puts the next kBits code bits
+// at bits 1..kBits, i.e. the byte address of their u16 table entry; one add of the
+// entry's step word then advances sh and prev together (the low byte stays in
+// [kCur - 63, kCur], so it never borrows from prev).
+template <bool kDelta, class Cfg, class Src>
+__device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut, uint32_t p,
+                                             uint32_t prev, __amdgpu_buffer_rsrc_t out,
+                                             uint32_t row0, uint32_t pitch, bool dead,
+                                             uint32_t prio = 0) {
   const uint8_t *wa = src.at((p >> 5) * 4u);
-  uint32_t S = (prev << 8) + 114u - (p & 31u);
+  uint32_t S = (prev << 8) + Cfg::kCur - (p & 31u);
   uint32_t hi = word_at(wa);
   uint32_t lo = word_at(wa + 4);
   uint32_t nw = word_at(wa + 8);
-  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
+  (void)prio;
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_LOOKUP(A1)                                                               \
   uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? 0u : (A1)));
 #define MH_FINISH(J, OW)                                                            \
   {                                                                                 \
-    const bool esc = e < kEscapeBelow;                                              \
-    if (__builtin_expect(__ballot(esc) != 0, 0)) {                                  \
-      const uint64_t x = (((uint64_t)hi) << 32) | lo;                               \
-      const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;                   \
-      const uint32_t e2 = s_lut[kL1Entries + ((e & 0xFFu) << kL2Bits) + x3];        \
-      e = esc ? e2 : e;                                                             \
+    if constexpr (Cfg::kEsc) {                                                      \
+      const bool esc = e < kEscapeBelow;                                            \
+      if (__builtin_expect(__ballot(esc) != 0, 0)) {                                \
+        const uint64_t x = (((uint64_t)hi) << 32) | lo;                             \
+        const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;                 \
+        const uint32_t e2 = *reinterpret_cast<const uint16_t *>(                    \
+            lut + 2u * (kL1Entries + ((e & 0xFFu) << kL2Bits) + x3));               \
+        e = esc ? e2 : e;                                                           \
+      }                                                                             \
     }                                                                               \
     S += e;                                                                         \
     if (kDelta) {                                                                   \
@@ -237,11 +291,10 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
       OW = __builtin_amdgcn_perm(e + 0x100u, OW, ins_sel1(J));                      \
     }                                                                               \
   }
-  // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_STEP(J, OW)                                                              \
   {                                                                                 \
     const uint64_t x = (((uint64_t)hi) << 32) | lo;                                 \
-    MH_LOOKUP((uint32_t)(x >> (S & 63u)) & 0x3FFEu)                                 \
+    MH_LOOKUP((uint32_t)(x >> (S & 63u)) & Cfg::kMask)                              \
     MH_FINISH(J, OW)                                                                \
   }
   // keep sh < 32 at the start of every symbol pair (each code is <= 16 bits)
@@ -254,27 +307,20 @@ __device__ __forceinline__ void decode_block(const Src &src, uint32_t p, uint32_
     S += d * 8u;                                                                    \
     nw = word_at(wa + 8);                                                           \
   }
-#if MH_SPEC_REFILL
-  // First symbol of a pair with the refill folded in: the table address is taken
-  // from whichever window the refill will select (both shifts run in parallel),
-  // so the word move itself overlaps the LDS read instead of preceding it.
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
-    const bool c = (S & 0xFFu) <= 82u;                                              \
-    const uint32_t v0 = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (S & 63u));    \
-    const uint32_t v1 = (uint32_t)(((((uint64_t)lo) << 32) | nw) >> ((S + 32u) & 63u)); \
-    MH_LOOKUP((c ? v1 : v0) & 0x3FFEu)                                              \
-    MH_REFILL_C(c)                                                                  \
-    MH_FINISH(J, OW)                                                                \
+    const bool c = (S & 0xFFu) <= Cfg::kRefillAt;                                   \
+    if constexpr (Cfg::kSpec) {                                                     \
+      const uint32_t v0 = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (S & 63u));  \
+      const uint32_t v1 = (uint32_t)(((((uint64_t)lo) << 32) | nw) >> ((S + 32u) & 63u)); \
+      MH_LOOKUP((c ? v1 : v0) & Cfg::kMask)                                         \
+      MH_REFILL_C(c)                                                                \
+      MH_FINISH(J, OW)                                                              \
+    } else {                                                                        \
+      MH_REFILL_C(c)                                                                \
+      MH_STEP(J, OW)                                                                \
+    }                                                                               \
   }
-#else
-#define MH_STEP_R(J, OW)                                                            \
-  {                                                                                 \
-    const bool c = (S & 0xFFu) <= 82u;                                              \
-    MH_REFILL_C(c)                                                                  \
-    MH_STEP(J, OW)                                                                  \
-  }
-#endif
 
 #if MH_ROW_UNROLL == 8
 #pragma unroll
@@ -460,10 +506,10 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Oversize tile: stage + decode lanes [0,32) then [32,64), each from its own span.
-template <bool kDelta>
+template <bool kDelta, class Cfg>
 __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t, uint32_t lane,
-                                                        uint8_t *stage, __amdgpu_buffer_rsrc_t out,
-                                                        uint32_t row0, bool dead) {
+                                              const uint8_t *lut, uint8_t *stage,
+                                              __amdgpu_buffer_rsrc_t out, uint32_t row0, bool dead) {
   const __amdgpu_buffer_rsrc_t rc = codes_rsrc(a, t);
   const uint32_t my_off = t.p + t.start * 8u;  // lane's absolute start bit
   const uint32_t fbits = t.fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : t.fb32 * 8u;
@@ -496,8 +542,8 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
     wave_sync();
     if (lane >= first && lane < first + 32u) {
       LdsWords src{stage};
-      decode_block<kDelta>(src, t.valid ? my_off - start * 8u : 0u, t.init, out, row0,
-                           (uint32_t)a.out_pitch, dead);
+      decode_block<kDelta, Cfg>(src, lut, t.valid ? my_off - start * 8u : 0u, t.init, out, row0,
+                                (uint32_t)a.out_pitch, dead);
     }
     wave_sync();
   }
@@ -516,6 +562,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   const uint32_t nwaves = blockDim.x >> 6;
   const uint32_t gstride = gridDim.x * nwaves;
   uint8_t *stage = s_stage + wave * kStageBytes;
+  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
 #if MH_DIAG_STAMPS
   unsigned long long ts[kDiagSlots] = {};
   bool first_tile = true;
@@ -579,7 +626,8 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
       // waves with more tiles left run first (the arbiter otherwise favours the oldest)
       set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
 #endif
-      decode_block<kDelta>(src, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead, prio);
+      decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
+                                  prio);
       prio += MH_PRIO_ROTATE == 2 ? 3u : 1u;
     }
 #if MH_DIAG_STAMPS
@@ -607,7 +655,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
     const __amdgpu_buffer_rsrc_t out =
         uniform_rsrc(a.out + (uint64_t)tt.f * a.out_frame_stride, a.out_frame_bytes);
-    decode_halves<kDelta>(a, tt, lane, stage, out, row0, !tt.valid);
+    decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, out, row0, !tt.valid);
   }
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
@@ -619,6 +667,64 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   if (lane == 0 && gw < (uint32_t)kDiagWaves)
     for (int i = 0; i < kDiagSlots; ++i) g_stamps[gw * kDiagSlots + i] = ts[i];
 #endif
+}
+
+// ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------
+// Every wave decodes one tile, so the per-symbol dependency chain (not LDS or VALU
+// throughput) sets the time: the step takes the refill off the chain (kSpec), and
+// when the table has no code longer than 14 bits the single-level 14-bit table
+// drops the escape test from it too.
+constexpr int kSmallMaxWaves = 4;
+__shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
+static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
+
+template <bool kDelta>
+__global__ void __launch_bounds__(64 * kSmallMaxWaves) mh_decode_small_kernel(const DecodeArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = blockDim.x >> 6;
+  uint8_t *stage = s_stage + wave * kStageBytes;
+  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut_small);
+  const uint8_t *prepared = reinterpret_cast<const uint8_t *>(a.lut);
+
+  const uint32_t max_len = *reinterpret_cast<const uint32_t *>(prepared + kMaxLenOff);  // scalar load
+  const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
+  TileHdr h;
+  hdr_issue(a, tile, lane, h);
+  const bool l14 = max_len <= (uint32_t)kLut14Bits;
+  {
+    const v4u32 *src = reinterpret_cast<const v4u32 *>(prepared + (l14 ? kLut14Off : 0));
+    v4u32 *dst = reinterpret_cast<v4u32 *>(s_lut_small);
+    const uint32_t n16 = (uint32_t)(l14 ? kLut14Bytes : kLutBytes) / 16u;
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  }
+  const Tile t = hdr_resolve(a, h, lane);
+  const bool live = t.tile < a.total_tiles;
+  const bool staged = live && t.span <= (uint32_t)kStageBytes;
+  v4u32 R[kStageChunks];
+  span_issue(a, t, lane, R, staged);
+  __syncthreads();  // table in LDS
+  if (!live) return;  // no barrier below
+  const uint32_t b = t.b0 + lane;
+  const uint32_t bx = b % a.bw, by = b / a.bw;
+  const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
+  const __amdgpu_buffer_rsrc_t out =
+      uniform_rsrc(a.out + (uint64_t)t.f * a.out_frame_stride, a.out_frame_bytes);
+  if (staged) {
+    span_write(t, lane, R, stage);
+    wave_sync();
+    LdsWords src{stage};
+    if (l14)
+      decode_block<kDelta, StepCfg<kLut14Bits, true>>(src, lut, t.p, t.init, out, row0,
+                                                      (uint32_t)a.out_pitch, !t.valid);
+    else
+      decode_block<kDelta, StepCfg<kLutBits, true>>(src, lut, t.p, t.init, out, row0,
+                                                    (uint32_t)a.out_pitch, !t.valid);
+  } else if (l14) {
+    decode_halves<kDelta, StepCfg<kLut14Bits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
+  } else {
+    decode_halves<kDelta, StepCfg<kLutBits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
+  }
 }
 
 int g_cu_count = 0;
@@ -654,6 +760,13 @@ int launch(const DecodeArgs &a0, hipStream_t s) {
   DecodeArgs a = a0;
   const int cus = cu_count();
   if (!cus) return MH_ERR_HIP;
+  if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxWaves * cus)) {
+    // one tile per wave, at most kSmallMaxWaves waves per CU
+    const uint32_t nw = (a.total_tiles + (uint32_t)cus - 1) / (uint32_t)cus;
+    a.n_groups = (a.total_tiles + nw - 1) / nw;
+    hipLaunchKernelGGL(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
+  }
   // Waves per workgroup: spread a small launch (one 2048x1536 frame = 768 tiles)
   // over every CU; 8-wave workgroups (3 per CU by LDS) for batches.
   uint32_t nw = (a.total_tiles + (uint32_t)cus - 1) / (uint32_t)cus;
@@ -678,7 +791,7 @@ int mh_diag_stamps(unsigned long long *host, size_t n) {
 }
 #endif
 
-size_t mh_lut_bytes(void) { return (size_t)kLutBytes; }
+size_t mh_lut_bytes(void) { return (size_t)kPreparedBytes; }
 int mh_lut_bits(void) { return kLutBits; }
 
 int mh_device_count(void) {
@@ -695,7 +808,8 @@ int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_t
   if ((uintptr_t)d_lut & 15u) return MH_ERR_ALIGN;
   hipLaunchKernelGGL(mh_prepare_lut_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint16_t *>(d_table1),
-                     reinterpret_cast<const uint16_t *>(d_table2), table2_entries, d_lut);
+                     reinterpret_cast<const uint16_t *>(d_table2), table2_entries,
+                     reinterpret_cast<uint8_t *>(d_lut));
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 

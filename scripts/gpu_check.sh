@@ -1,13 +1,14 @@
-# GPU round check: parity tests, smoke, bench, rocprofv3 kernel trace.
+# GPU round check: parity tests, smoke, bench, rocprofv3 kernel trace (fail-fast).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest rc=$?"
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-echo "smoke rc=$?"
-timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
-echo "bench rc=$?"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
-echo "rocprof rc=$?"
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
+echo "smoke ok"
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || { tail gpurun_out/bench_prof.err; exit 1; }
+python3 scripts/ktrace_summary.py gpurun_out/prof > gpurun_out/ktrace_summary.txt && cat gpurun_out/ktrace_summary.txt
