@@ -130,6 +130,20 @@ int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_t
 /* Number of LUT index bits used by the kernel (first-level lookup width). */
 int mh_lut_bits(void);
 
+/* GPU-side table build from the 256-byte canonical header (the device twin of
+ * mh_build_tables: HuffmanUtil.cpp:270-310 parseCanonicalHeader + :338-667
+ * generateSplitLookupTables 8/8). Writes T1 (256 entries), T2 through its full
+ * MH_TABLE2_MAX_ENTRIES capacity (zero beyond the (k+1)*256 used entries, so
+ * mh_decode may be given table2_entries = MH_TABLE2_MAX_ENTRIES), the used entry
+ * count to *d_table2_entries, and -- when d_lut is non-NULL -- the prepared
+ * table (mh_prepare_lut). d_status (optional, device int32): MH_OK, or
+ * MH_ERR_CODE_TOO_LONG / MH_ERR_TABLE (lengths that are not a prefix code), in
+ * which case the tables are left zero. All pointers are device pointers;
+ * asynchronous on `stream`. Lets a multi-GPU job broadcast 256 bytes. */
+int mh_build_tables_device(const uint8_t *d_canon_header, mh_lookup_symbol *d_table1,
+                           mh_lookup_symbol *d_table2, uint32_t *d_table2_entries,
+                           uint16_t *d_lut, int32_t *d_status, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Host-side producer (CPU, reentrant). Outputs are byte-identical to the   */
 /* reference's C++ codec.                                                   */

@@ -23,6 +23,7 @@ EXPORTS = (
     "mh_merge_blocks", "mh_encode_signed_byte_deltas", "mh_decode_signed_byte_deltas",
     "mh_codes_bound", "mh_encode_huffman", "mh_encode_frame", "mh_canonical_codes",
     "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
+    "mh_build_tables_device",
 )
 
 
@@ -76,6 +77,7 @@ def lib() -> ctypes.CDLL:
         L.mh_lut_bytes.restype = ctypes.c_size_t
         L.mh_lut_bits.restype = ctypes.c_int
         L.mh_prepare_lut.argtypes = [_vp, _vp, ctypes.c_uint32, _vp, _vp]
+        L.mh_build_tables_device.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
         L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint8, _u8p, ctypes.c_size_t]
         L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

@@ -24,6 +24,8 @@ ARCH = os.environ.get("MH_OFFLOAD_ARCH", "gfx950")
 SOURCES = {
     "mh_decode.o": ("mh_decode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
+    "mh_tables.o": ("mh_tables.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+                                      "-Wall", "-c"]),
     "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),
 }
 HEADERS = [os.path.join(ROOT, "include", "metalhuffman.h")]

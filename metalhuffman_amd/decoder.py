@@ -55,6 +55,42 @@ class DeviceTables:
             tabs.prepare_lut(stream)
         return tabs
 
+    @classmethod
+    def from_canonical_header(cls, canon, device="cuda", prepare_lut: bool = True,
+                              stream: Optional[torch.cuda.Stream] = None) -> "DeviceTables":
+        """Build T1/T2 (and the prepared table) ON the device from the 256-byte
+        canonical header (mh_build_tables_device), e.g. after a 256-byte broadcast.
+        T2 keeps its full MH_TABLE2_MAX_ENTRIES capacity (zero past the used
+        subtables). Asynchronous; check_status() syncs and raises on a bad header."""
+        dev = _dev(device)
+        if isinstance(canon, torch.Tensor):
+            hdr = canon.to(dev, torch.uint8).contiguous()
+        else:
+            hdr = torch.from_numpy(np.ascontiguousarray(canon, np.uint8)).to(dev)
+        if hdr.numel() != 256:
+            raise ValueError("the canonical header has 256 entries")
+        d1 = torch.empty(512, dtype=torch.uint8, device=dev)
+        d2 = torch.empty(2 * N.MH_TABLE2_MAX_ENTRIES, dtype=torch.uint8, device=dev)
+        meta = torch.zeros(2, dtype=torch.int32, device=dev)  # [used T2 entries, status]
+        lut = torch.empty(int(N.lib().mh_lut_bytes()), dtype=torch.uint8, device=dev) if prepare_lut else None
+        N.check(N.lib().mh_build_tables_device(hdr.data_ptr(), d1.data_ptr(), d2.data_ptr(),
+                                               meta.data_ptr(), lut.data_ptr() if lut is not None else None,
+                                               meta.data_ptr() + 4, _stream_ptr(stream, dev)),
+                "mh_build_tables_device")
+        tabs = cls(d1, d2, lut)
+        tabs._meta = meta
+        return tabs
+
+    def check_status(self) -> int:
+        """Used T2 entries of a device-built table (synchronises); raises MHError
+        when the header was rejected."""
+        meta = getattr(self, "_meta", None)
+        if meta is None:
+            return self.table2_entries
+        entries, status = (int(v) for v in meta.cpu().tolist())
+        N.check(status, "mh_build_tables_device")
+        return entries
+
     def prepare_lut(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         dev = self.table1.device
         lut = torch.empty(int(N.lib().mh_lut_bytes()), dtype=torch.uint8, device=dev)

@@ -91,6 +91,8 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_decode(ctypes.byref(_frame()), 0x50000, 1024, 0, None) == -4    # pitch < width
     assert L.mh_prepare_lut(0x30000, 0x40000, 300, 0x60000, None) == -5
     assert L.mh_prepare_lut(None, 0x40000, 256, 0x60000, None) == -1
+    assert L.mh_build_tables_device(None, 0x30000, 0x40000, 0x50000, None, None, None) == -1
+    assert L.mh_build_tables_device(0x10000, 0x30000, 0x40000, 0x50000, 0x60004, None, None) == -6
 
 
 def test_constants(mh):
