@@ -161,14 +161,22 @@ def measured_traffic(workload: str):
         return None
 
 
-def roofline(bytes_per_launch, kernel_ms, workload=None):
-    avg_s = float(np.mean(kernel_ms)) * 1e-3
+def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
+    """achieved = algorithmic bytes of one launch / the launch's average duration,
+    the latter from the HIP events bracketing the timed hipGraph replay on its
+    stream (the K kernels run back to back there, so region / K is the kernel
+    duration rocprofv3's kernel trace reports for the same command)."""
+    avg_s = region_ms * 1e-3 / steps
     ach = bytes_per_launch / avg_s / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": measured_traffic(workload) if workload else None,
-            "kernel_us_avg": round(avg_s * 1e6, 3), "kernel_us_median": round(float(np.median(kernel_ms)) * 1e3, 3),
-            "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4),
+         "traffic": measured_traffic(workload) if workload else None,
+         "kernel_us_avg": round(avg_s * 1e6, 3),
+         "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    if eager_ms:
+        # one launch at a time with an event pair each (includes launch latency)
+        r["eager_launch_us_median"] = round(float(np.median(eager_ms)) * 1e3, 3)
+    return r
 
 
 def cpu_baseline(efs, threads):
@@ -231,20 +239,19 @@ def main(argv=None) -> int:
     # shared table: built on rank 0, broadcast over RCCL
     t_bcast_us = None
     if world > 1:
-        t1 = t2 = None
-        if rank == 0:
-            t1, t2 = mh.encode_frame(bb).tables()
+        # 256-byte canonical header over RCCL; each GPU builds T1/T2 + its decode table
+        canon = mh.encode_frame(bb).canon if rank == 0 else None
         torch.cuda.synchronize(dev)
+        dist.barrier()
         tb = time.perf_counter()
-        d1, d2 = MD.broadcast_tables(t1, t2, src=0, device=dev)
+        tables = MD.broadcast_header_device_tables(canon, src=0, device=dev)
         torch.cuda.synchronize(dev)
         t_bcast_us = (time.perf_counter() - tb) * 1e6
-        tables = D.DeviceTables(d1.clone(), d2.clone(), None)
-        tables.prepare_lut()
+        tables.check_status()
     else:
         t1, t2 = mh.encode_frame(bb).tables()
         tables = D.DeviceTables.upload(t1, t2, dev)
-    t2_bytes = tables.table2.numel()
+    t2_bytes = 2 * tables.check_status()  # used T2 bytes (a device-built T2 keeps full capacity)
 
     # this rank's resident frames (distinct block shuffles: one shared table)
     seeds = [rank * args.frames + i for i in range(args.frames)]
@@ -306,26 +313,28 @@ def main(argv=None) -> int:
                    "frames_per_step_per_gpu": int(wl.launches[0].n_frames),
                    "parallelism": f"frame-sharded x{world}", "launch": "hipGraph" if not args.no_graph else "eager"},
         "mpixels_per_s": round(value, 1),
-        "roofline": roofline(wl.bytes, kms, args.workload),
+        "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload),
         "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
     }
     if t_bcast_us is not None:
-        result["table_broadcast_us"] = round(t_bcast_us, 1)
+        result["table_broadcast_us"] = round(t_bcast_us, 1)  # 256-B RCCL broadcast + device table build
+        result["table_broadcast_bytes"] = 256
 
     if world == 1 and rank == 0 and not args.no_extras:
         extras = {}
-        for name, make, steps, key in (("batch64", lambda: batch_workload(args.batch), 20, "batch"),
-                                       ("tile8192", tile_workload, 20, "tile8192")):
+        # ~20 ms of launches each, after a warm-up of the same length (clocks settle)
+        for name, make, steps, key in (("batch64", lambda: batch_workload(args.batch), 256, "batch"),
+                                       ("tile8192", tile_workload, 512, "tile8192")):
             if name.startswith("batch") and args.workload == "batch":
                 continue
             if name == "tile8192" and args.workload == "tile8192":
                 continue
             w2 = make()
-            wall2, reg2, kms2 = w2.run(steps, 3, use_graph=not args.no_graph)
+            wall2, reg2, kms2 = w2.run(steps, steps, use_graph=not args.no_graph)
             extras[name] = {"value_MBps": round(w2.pixels / (wall2 / steps) / 1e6, 1),
                             "ms_per_step": round(wall2 / steps * 1e3, 4),
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
-                            "roofline": roofline(w2.bytes, kms2, key)}
+                            "roofline": roofline(w2.bytes, reg2, steps, kms2, key)}
             del w2
         result["extras"] = extras
 

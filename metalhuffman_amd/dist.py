@@ -2,10 +2,11 @@
 
 Frames are independent (each carries its own block offsets), so the batch is split
 into contiguous per-rank frame ranges with no data-path collective. The only
-exchange is the shared symbol table: rank 0 broadcasts T1||T2 (BigBridge: 512 +
-14,848 bytes) -- or the 256-byte canonical header every rank can rebuild the tables
-from -- over torch.distributed. With backend "nccl" on ROCm that is RCCL over xGMI;
-with "gloo" (tests) it runs on the CPU.
+exchange is the shared symbol table: rank 0 broadcasts the 256-byte canonical
+header and every GPU rebuilds T1/T2 and its decode table on the device
+(broadcast_header_device_tables), or rank 0 broadcasts T1||T2 itself (BigBridge:
+512 + 14,848 bytes). With backend "nccl" on ROCm that is RCCL over xGMI; with
+"gloo" (tests) it runs on the CPU.
 """
 from __future__ import annotations
 
@@ -58,3 +59,19 @@ def broadcast_canonical_header(canon: np.ndarray | None, src: int = 0,
     canon_all = buf.cpu().numpy()
     t1, t2 = Huffman.generateSplitLookupTables(canon_all)
     return canon_all, t1, t2
+
+
+def broadcast_header_device_tables(canon: np.ndarray | None, src: int = 0,
+                                   device: torch.device | str = "cuda", group=None):
+    """Broadcast the 256-byte canonical header from `src` straight into device
+    memory and build T1/T2 + the prepared decode table there
+    (mh_build_tables_device): one 256-byte RCCL broadcast per table change."""
+    from .decoder import DeviceTables
+    device = torch.device(device)
+    # RCCL broadcasts device memory; gloo (CPU tests) a host tensor
+    on = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    buf = torch.empty(256, dtype=torch.uint8, device=on)
+    if dist.get_rank(group) == src:
+        buf.copy_(torch.from_numpy(np.ascontiguousarray(canon, np.uint8)))
+    dist.broadcast(buf, src=src, group=group)
+    return DeviceTables.from_canonical_header(buf, device)
