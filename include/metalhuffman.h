@@ -145,6 +145,38 @@ int mh_build_tables_device(const uint8_t *d_canon_header, mh_lookup_symbol *d_ta
                            uint16_t *d_lut, int32_t *d_status, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* Streaming from host memory (BASELINE config 5; the reference's per-frame  */
+/* command buffer, AAPLRenderer.m:1178-1921).                               */
+
+typedef struct mh_stream mh_stream;
+
+/* A decode stream for frames shaped like `proto` (dims, flags, tables, d_lut;
+ * a non-NULL proto->d_block_init means frames carry per-block init bytes; the
+ * frame pointers in proto are ignored). It owns n_slots device slots of
+ * codes_capacity code bytes each, a copy stream and a compute stream, and one
+ * captured decode graph per slot. Slot i decodes into d_outputs[i] (caller
+ * device buffers of round_up(W, 8) * H bytes, 8-byte aligned) or, when
+ * d_outputs is NULL, into rasters the stream allocates. */
+int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_slots,
+                     uint8_t *const *d_outputs, mh_stream **out);
+/* Queue one frame: H2D copy of its host buffers (pinned memory for a DMA) into
+ * the next slot once that slot's previous decode is done, then the slot's
+ * decode. codes_bytes includes the MH_CODES_PAD zero bytes; h_block_init must
+ * be given iff the stream was created with it. When the host codes follow the
+ * block offsets at byte round_up(4*NB, 16) of one buffer, both move in one DMA.
+ * Returns the slot in *slot. */
+int mh_stream_submit(mh_stream *s, const uint8_t *h_codes, uint64_t codes_bytes,
+                     const uint32_t *h_block_offsets, const uint8_t *h_block_init,
+                     uint32_t *slot);
+/* The slot's output raster (device); valid until n_slots further submits. */
+uint8_t *mh_stream_output(mh_stream *s, uint32_t slot, size_t *out_pitch);
+/* The stream's compute stream (hipStream_t), for events or dependent work. */
+void *mh_stream_compute_stream(mh_stream *s);
+int mh_stream_wait(mh_stream *s, uint32_t slot);  /* that slot's decode done */
+int mh_stream_synchronize(mh_stream *s);
+int mh_stream_destroy(mh_stream *s);
+
+/* ---------------------------------------------------------------------- */
 /* Host-side producer (CPU, reentrant). Outputs are byte-identical to the   */
 /* reference's C++ codec.                                                   */
 

@@ -23,7 +23,8 @@ EXPORTS = (
     "mh_merge_blocks", "mh_encode_signed_byte_deltas", "mh_decode_signed_byte_deltas",
     "mh_codes_bound", "mh_encode_huffman", "mh_encode_frame", "mh_canonical_codes",
     "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
-    "mh_build_tables_device",
+    "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
+    "mh_stream_compute_stream", "mh_stream_wait", "mh_stream_synchronize", "mh_stream_destroy",
 )
 
 
@@ -78,6 +79,16 @@ def lib() -> ctypes.CDLL:
         L.mh_lut_bits.restype = ctypes.c_int
         L.mh_prepare_lut.argtypes = [_vp, _vp, ctypes.c_uint32, _vp, _vp]
         L.mh_build_tables_device.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        L.mh_stream_create.argtypes = [ctypes.POINTER(mh_frame), ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.POINTER(_vp), ctypes.POINTER(_vp)]
+        L.mh_stream_submit.argtypes = [_vp, _vp, ctypes.c_uint64, _vp, _vp, _u32p]
+        L.mh_stream_output.argtypes = [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]
+        L.mh_stream_output.restype = _vp
+        L.mh_stream_compute_stream.argtypes = [_vp]
+        L.mh_stream_compute_stream.restype = _vp
+        L.mh_stream_wait.argtypes = [_vp, ctypes.c_uint32]
+        L.mh_stream_synchronize.argtypes = [_vp]
+        L.mh_stream_destroy.argtypes = [_vp]
         L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint8, _u8p, ctypes.c_size_t]
         L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

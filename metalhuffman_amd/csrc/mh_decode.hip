@@ -445,7 +445,9 @@ __device__ __forceinline__ Tile hdr_resolve(const DecodeArgs &a, const TileHdr &
   }
   t.fb32 = (uint32_t)(fbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : fbytes);
   const uint32_t fbits = t.fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : t.fb32 * 8u;
-  const uint32_t end_l = (b + 1u < a.nb) ? h.nxt : fbits;
+  // a frame's last block ends at most 64 x 16 bits after its start, whatever the
+  // buffer size (a reused streaming slot is larger than the frame it holds)
+  const uint32_t end_l = (b + 1u < a.nb) ? h.nxt : min(fbits, h.off + 64u * 16u);
   const uint32_t last = min(63u, a.nb - 1u - t.b0);  // last lane holding a block
   const uint32_t sb = __builtin_amdgcn_readfirstlane(h.off);
   const uint32_t eb = __builtin_amdgcn_readlane(end_l, last);

@@ -1,0 +1,235 @@
+// mh_stream.cpp -- frames streamed from host memory (BASELINE config 5, SURVEY.md
+// 8(f) rank 2): the native analogue of the reference's per-frame command buffer
+// (Shared/AAPLRenderer.m:1178-1921, one decode per drawInMTKView).
+//
+// A stream owns `slots` device slots (codes, block offsets, optional per-block
+// init bytes, output raster). mh_stream_submit copies one frame's host buffers
+// into the next slot on a copy stream (hipMemcpyAsync; pinned host memory makes
+// it a DMA) and replays that slot's captured decode graph on a compute stream,
+// so the copy of frame i+1 overlaps the decode of frame i. A slot is reused only
+// after its previous decode has finished (event wait on the copy stream), and its
+// output stays valid until `slots` further submits.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/metalhuffman.h"
+
+struct mh_stream {
+  struct Slot {
+    uint8_t *base = nullptr;    // [block offsets, padded to 16 B][codes]
+    uint8_t *codes = nullptr;
+    uint32_t *offsets = nullptr;
+    uint8_t *init = nullptr;
+    uint8_t *out = nullptr;
+    bool own_out = true;
+    hipEvent_t copied = nullptr, done = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    bool used = false;
+  };
+  int device = 0;
+  hipStream_t copy = nullptr, compute = nullptr;
+  mh_frame proto{};
+  uint64_t cap = 0;
+  uint64_t nb = 0;
+  uint64_t off_bytes = 0;  // nb * 4 rounded up to 16
+  size_t pitch = 0, out_bytes = 0;
+  uint32_t next = 0;
+  bool graphs = true;
+  std::vector<Slot> slots;
+};
+
+namespace {
+
+void release(mh_stream *s) {
+  if (!s) return;
+  for (auto &sl : s->slots) {
+    if (sl.exec) (void)hipGraphExecDestroy(sl.exec);
+    if (sl.graph) (void)hipGraphDestroy(sl.graph);
+    if (sl.copied) (void)hipEventDestroy(sl.copied);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    (void)hipFree(sl.base);
+    (void)hipFree(sl.init);
+    if (sl.own_out) (void)hipFree(sl.out);
+  }
+  if (s->copy) (void)hipStreamDestroy(s->copy);
+  if (s->compute) (void)hipStreamDestroy(s->compute);
+  delete s;
+}
+
+bool decode_slot(mh_stream *s, mh_stream::Slot &sl) {
+  mh_frame f = s->proto;
+  f.d_codes = sl.codes;
+  f.codes_bytes = s->cap;
+  f.d_block_offsets = sl.offsets;
+  f.d_block_init = sl.init;
+  return mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute) == MH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_slots,
+                     uint8_t *const *d_outputs, mh_stream **out) {
+  if (!proto || !out || !proto->d_table1 || !proto->d_table2 || n_slots < 1 || n_slots > 64 ||
+      codes_capacity < MH_CODES_PAD)
+    return MH_ERR_INVALID_ARG;
+  const mh_dims &d = proto->dims;
+  if (!d.width || !d.height || d.width > MH_MAX_DIM || d.height > MH_MAX_DIM ||
+      d.block_width != (d.width + 7) / 8 || d.block_height != (d.height + 7) / 8)
+    return MH_ERR_DIMS;
+  *out = nullptr;
+  mh_stream *s = new (std::nothrow) mh_stream();
+  if (!s) return MH_ERR_CAPACITY;
+  s->proto = *proto;
+  s->proto.n_frames = 1;
+  s->proto.d_frame_code_offsets = nullptr;
+  s->cap = (codes_capacity + 15) & ~15ull;
+  s->nb = (uint64_t)d.block_width * d.block_height;
+  s->off_bytes = (s->nb * 4 + 15) & ~15ull;
+  s->pitch = ((size_t)d.width + 7) & ~(size_t)7;
+  s->out_bytes = s->pitch * d.height;
+  s->slots.resize(n_slots);
+  const bool want_init = proto->d_block_init != nullptr;
+  // MH_STREAM_GRAPHS=0: direct launches instead of per-slot graph replays (A/B)
+  const char *ge = std::getenv("MH_STREAM_GRAPHS");
+  s->graphs = !(ge && ge[0] == '0');
+  int rc = MH_OK;
+  if (hipGetDevice(&s->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->compute, hipStreamNonBlocking) != hipSuccess)
+    rc = MH_ERR_HIP;
+  for (uint32_t i = 0; i < n_slots && rc == MH_OK; ++i) {
+    mh_stream::Slot &sl = s->slots[i];
+    if (d_outputs) {
+      sl.out = d_outputs[i];
+      sl.own_out = false;
+      if (!sl.out || ((uintptr_t)sl.out & 7u)) {
+        rc = MH_ERR_ALIGN;
+        break;
+      }
+    }
+    if (hipMalloc(&sl.base, s->off_bytes + s->cap) != hipSuccess ||
+        (want_init && hipMalloc(&sl.init, s->nb) != hipSuccess) ||
+        (!d_outputs && hipMalloc(&sl.out, s->out_bytes) != hipSuccess) ||
+        hipMemset(sl.base, 0, s->off_bytes + s->cap) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+      rc = MH_ERR_HIP;
+      break;
+    }
+    sl.offsets = reinterpret_cast<uint32_t *>(sl.base);
+    sl.codes = sl.base + s->off_bytes;
+    if (want_init && hipMemset(sl.init, 0, s->nb) != hipSuccess) {
+      rc = MH_ERR_HIP;
+      break;
+    }
+    // The decode of this slot, captured once: the slot's buffers never move, and
+    // codes_bytes = the slot capacity (the kernel bounds a frame's last block by
+    // its 64 x 16-bit maximum, not by the buffer end).
+    mh_frame f = s->proto;
+    f.d_codes = sl.codes;
+    f.codes_bytes = s->cap;
+    f.d_block_offsets = sl.offsets;
+    f.d_block_init = sl.init;
+    // one eager decode first: validates the arguments and caches the launch
+    // geometry queries outside the capture
+    const int wrc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute);
+    if (wrc != MH_OK) {
+      rc = wrc;
+      break;
+    }
+    if (!s->graphs) continue;
+    if (hipStreamBeginCapture(s->compute, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      rc = MH_ERR_HIP;
+      break;
+    }
+    const int drc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s->compute, &g);
+    sl.graph = g;
+    if (drc != MH_OK || e != hipSuccess) {
+      rc = drc != MH_OK ? drc : MH_ERR_HIP;
+      break;
+    }
+    if (hipGraphInstantiate(&sl.exec, sl.graph, nullptr, nullptr, 0) != hipSuccess) {
+      rc = MH_ERR_HIP;
+      break;
+    }
+  }
+  if (rc == MH_OK && hipDeviceSynchronize() != hipSuccess) rc = MH_ERR_HIP;
+  if (rc != MH_OK) {
+    release(s);
+    return rc;
+  }
+  *out = s;
+  return MH_OK;
+}
+
+int mh_stream_submit(mh_stream *s, const uint8_t *h_codes, uint64_t codes_bytes,
+                     const uint32_t *h_block_offsets, const uint8_t *h_block_init,
+                     uint32_t *slot_out) {
+  if (!s || !h_codes || !h_block_offsets) return MH_ERR_INVALID_ARG;
+  if (codes_bytes < MH_CODES_PAD || codes_bytes > s->cap) return MH_ERR_CAPACITY;
+  if (!h_block_init != !s->slots[0].init) return MH_ERR_INVALID_ARG;
+  const uint32_t k = s->next;
+  mh_stream::Slot &sl = s->slots[k];
+  // the slot's previous decode must be done before its buffers are overwritten
+  if (sl.used && hipStreamWaitEvent(s->copy, sl.done, 0) != hipSuccess) return MH_ERR_HIP;
+  // host offsets and codes laid out like the slot ([offsets, padded to 16 B][codes]):
+  // one DMA; otherwise two
+  const bool packed = h_codes == reinterpret_cast<const uint8_t *>(h_block_offsets) + s->off_bytes;
+  if ((packed ? hipMemcpyAsync(sl.base, h_block_offsets, s->off_bytes + codes_bytes,
+                               hipMemcpyHostToDevice, s->copy) != hipSuccess
+              : (hipMemcpyAsync(sl.codes, h_codes, codes_bytes, hipMemcpyHostToDevice, s->copy) !=
+                     hipSuccess ||
+                 hipMemcpyAsync(sl.offsets, h_block_offsets, s->nb * 4, hipMemcpyHostToDevice,
+                                s->copy) != hipSuccess)) ||
+      (h_block_init &&
+       hipMemcpyAsync(sl.init, h_block_init, s->nb, hipMemcpyHostToDevice, s->copy) != hipSuccess) ||
+      hipEventRecord(sl.copied, s->copy) != hipSuccess ||
+      hipStreamWaitEvent(s->compute, sl.copied, 0) != hipSuccess ||
+      (s->graphs ? hipGraphLaunch(sl.exec, s->compute) != hipSuccess : !decode_slot(s, sl)) ||
+      hipEventRecord(sl.done, s->compute) != hipSuccess)
+    return MH_ERR_HIP;
+  sl.used = true;
+  s->next = (k + 1) % (uint32_t)s->slots.size();
+  if (slot_out) *slot_out = k;
+  return MH_OK;
+}
+
+uint8_t *mh_stream_output(mh_stream *s, uint32_t slot, size_t *out_pitch) {
+  if (!s || slot >= s->slots.size()) return nullptr;
+  if (out_pitch) *out_pitch = s->pitch;
+  return s->slots[slot].out;
+}
+
+void *mh_stream_compute_stream(mh_stream *s) { return s ? (void *)s->compute : nullptr; }
+
+int mh_stream_wait(mh_stream *s, uint32_t slot) {
+  if (!s || slot >= s->slots.size()) return MH_ERR_INVALID_ARG;
+  if (!s->slots[slot].used) return MH_OK;
+  return hipEventSynchronize(s->slots[slot].done) == hipSuccess ? MH_OK : MH_ERR_HIP;
+}
+
+int mh_stream_synchronize(mh_stream *s) {
+  if (!s) return MH_ERR_INVALID_ARG;
+  return (hipStreamSynchronize(s->copy) == hipSuccess && hipStreamSynchronize(s->compute) == hipSuccess)
+             ? MH_OK
+             : MH_ERR_HIP;
+}
+
+int mh_stream_destroy(mh_stream *s) {
+  if (!s) return MH_ERR_INVALID_ARG;
+  const int rc = mh_stream_synchronize(s);
+  release(s);
+  return rc;
+}
+
+}  // extern "C"

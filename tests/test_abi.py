@@ -93,6 +93,12 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_prepare_lut(None, 0x40000, 256, 0x60000, None) == -1
     assert L.mh_build_tables_device(None, 0x30000, 0x40000, 0x50000, None, None, None) == -1
     assert L.mh_build_tables_device(0x10000, 0x30000, 0x40000, 0x50000, 0x60004, None, None) == -6
+    h = ctypes.c_void_p()
+    assert L.mh_stream_create(None, 4096, 2, None, ctypes.byref(h)) == -1
+    assert L.mh_stream_create(ctypes.byref(_frame()), 4096, 0, None, ctypes.byref(h)) == -1
+    assert L.mh_stream_create(ctypes.byref(_frame(dims=N.mh_dims(16, 16, 3, 2))), 4096, 2, None,
+                              ctypes.byref(h)) == -2
+    assert L.mh_stream_submit(None, 0x1000, 4096, 0x2000, None, None) == -1
 
 
 def test_constants(mh):

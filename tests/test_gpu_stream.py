@@ -1,0 +1,46 @@
+"""Config 5 (frames streamed from host memory): the native double-buffered stream
+(mh_stream_*) must deliver every frame bit-exactly, with slots reused in turn and
+per-block init bytes carried when the stream is created with them."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(mh, device, imgs, init_zero=False, slots=2):
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd.stream import FrameStream, pinned_frame
+    efs = [mh.encode_frame(im, init_zero_delta=init_zero) for im in imgs]
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    h, w = imgs[0].shape
+    cap = max(ef.codes.size for ef in efs)
+    fs = FrameStream(tabs, w, h, cap, slots=slots, block_init=init_zero, device=device)
+    hosts = [pinned_frame(ef) for ef in efs]
+    inits = [torch.from_numpy(ef.block_init).pin_memory() for ef in efs] if init_zero else None
+    pending = []
+    for i, (c, o) in enumerate(hosts):
+        slot = fs.submit(c, o, inits[i] if init_zero else None)
+        pending.append((i, slot))
+        if len(pending) == slots:          # oldest frame: wait, check before its slot is reused
+            j, sj = pending.pop(0)
+            fs.wait(sj)
+            assert np.array_equal(fs.output(sj)[:, :w].cpu().numpy(), imgs[j]), j
+    fs.synchronize()
+    for j, sj in pending:
+        assert np.array_equal(fs.output(sj)[:, :w].cpu().numpy(), imgs[j]), j
+    fs.close()
+
+
+def test_stream_double_buffered(mh, device, bigbridge):
+    from metalhuffman_amd import frames as F
+    _run(mh, device, [F.block_shuffle(bigbridge, 60 + s) for s in range(10)])
+
+
+def test_stream_three_slots_odd_size_init_bytes(mh, device, bigbridge):
+    from metalhuffman_amd import frames as F
+    base = np.ascontiguousarray(bigbridge[:768, :1000])
+    _run(mh, device, [F.block_shuffle(base, s) for s in range(7)], init_zero=True, slots=3)
