@@ -145,6 +145,28 @@ int mh_build_tables_device(const uint8_t *d_canon_header, mh_lookup_symbol *d_ta
                            uint16_t *d_lut, int32_t *d_status, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* GPU encoder (the producer side on the device; output byte-identical to   */
+/* mh_encode_frame: HuffmanEncoder.cpp:310-381, HuffmanUtil.cpp:1051-1131,  */
+/* AAPLRenderer.m:374-688).                                                 */
+
+/* Device workspace mh_encode_frame_device needs for a width x height frame. */
+size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height);
+
+/* Encode the device frame d_gray (W x H bytes, row stride W): block split,
+ * deltas (unless MH_FLAG_NO_DELTA) and histogram on the device, the Huffman
+ * tree on the host from the 256 counts, then canonical codes, block offsets (a
+ * prefix sum of per-block bit lengths) and MSB-first bit packing on the device.
+ * Writes canon_header (host), d_codes (4-byte aligned; *codes_len = payload +
+ * MH_CODES_PAD zero bytes, codes_cap >= round_up(*codes_len, 4)),
+ * d_block_offsets (u32[NB]) and, if non-NULL, d_block_init (u8[NB], the
+ * IMPL_DELTAS_AND_INIT_ZERO_DELTA variant). d_workspace: 256-byte aligned,
+ * mh_encode_workspace_bytes(). Synchronises `stream` once (the histogram). */
+int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
+                           uint8_t canon_header[256], uint8_t *d_codes, uint64_t codes_cap,
+                           uint64_t *codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                           void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------- */
 /* Streaming from host memory (BASELINE config 5; the reference's per-frame  */
 /* command buffer, AAPLRenderer.m:1178-1921).                               */
 
@@ -224,6 +246,11 @@ int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]);
  * room for MH_TABLE2_MAX_ENTRIES entries; *table2_entries = (k+1)*256. */
 int mh_build_tables(const uint8_t canon_header[256], mh_lookup_symbol table1[256],
                     mh_lookup_symbol *table2, uint32_t table2_cap, uint32_t *table2_entries);
+
+/* Huffman code lengths (the canonical header) from 256 symbol counts, with the
+ * reference tree's tie-breaking (HuffmanEncoder.cpp:29-145). MH_ERR_EMPTY for no
+ * symbols, MH_ERR_CODE_TOO_LONG past 16 bits (lengths still written). */
+int mh_code_lengths(const uint64_t freq[256], uint8_t canon_header[256]);
 
 /* HuffmanUtil::generateLookupTable (HuffmanUtil.cpp:314-334): 65536 entries. */
 int mh_build_single_table(const uint8_t canon_header[256], mh_lookup_symbol table[65536]);

@@ -25,6 +25,7 @@ EXPORTS = (
     "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
     "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
     "mh_stream_compute_stream", "mh_stream_wait", "mh_stream_synchronize", "mh_stream_destroy",
+    "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
 )
 
 
@@ -89,6 +90,12 @@ def lib() -> ctypes.CDLL:
         L.mh_stream_wait.argtypes = [_vp, ctypes.c_uint32]
         L.mh_stream_synchronize.argtypes = [_vp]
         L.mh_stream_destroy.argtypes = [_vp]
+        L.mh_code_lengths.argtypes = [_u64p, _u8p]
+        L.mh_encode_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.mh_encode_workspace_bytes.restype = ctypes.c_size_t
+        L.mh_encode_frame_device.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
+                                             _vp, ctypes.c_uint64, _u64p, _vp, _vp, _vp, ctypes.c_size_t,
+                                             _vp]
         L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint8, _u8p, ctypes.c_size_t]
         L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

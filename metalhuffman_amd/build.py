@@ -26,6 +26,8 @@ SOURCES = {
                                       "-Wall", "-c"]),
     "mh_tables.o": ("mh_tables.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
+    "mh_encode.o": ("mh_encode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+                                      "-Wall", "-c"]),
     "mh_stream.o": ("mh_stream.cpp", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
     "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),

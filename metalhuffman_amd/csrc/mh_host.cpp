@@ -255,6 +255,11 @@ int mh_encode_frame(const uint8_t *gray, uint32_t width, uint32_t height, uint32
   return MH_OK;
 }
 
+int mh_code_lengths(const uint64_t freq[256], uint8_t canon_header[256]) {
+  if (!freq || !canon_header) return MH_ERR_INVALID_ARG;
+  return code_lengths(freq, canon_header);
+}
+
 int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]) {
   if (!canon_header || !codes) return MH_ERR_INVALID_ARG;
   for (int s = 0; s < 256; ++s)

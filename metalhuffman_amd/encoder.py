@@ -1,0 +1,76 @@
+"""GPU encoder: a device frame in, the reference's buffers out (mh_encode_frame_device).
+
+Byte-identical to the host codec (codec.encode_frame), so frames encoded on the GPU
+feed the decoder -- and the reference's own renderer contract -- unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .codec import block_grid
+from .decoder import DeviceFrames, _dev, _stream_ptr
+
+
+@dataclasses.dataclass
+class DeviceEncodedFrame:
+    width: int
+    height: int
+    canon: np.ndarray                 # u8[256] canonical header (host)
+    codes: torch.Tensor               # u8[codes_len] on the device (payload + 4 zero bytes)
+    block_offsets: torch.Tensor       # int32 view of u32[NB] on the device
+    block_init: Optional[torch.Tensor]
+    flags: int
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.codes.numel()) - N.MH_CODES_PAD
+
+    def frames(self) -> DeviceFrames:
+        """The encoded frame as a one-frame DeviceFrames for decode()."""
+        return DeviceFrames(self.width, self.height, 1, self.block_offsets, self.codes, None,
+                            self.block_init, self.flags, self.payload_bytes)
+
+
+class Encoder:
+    """Reusable device workspace + output buffers for frames of one size."""
+
+    def __init__(self, width: int, height: int, device="cuda"):
+        self.device = _dev(device)
+        self.width, self.height = width, height
+        bw, bh = block_grid(width, height)
+        self.nb = bw * bh
+        ws = int(N.lib().mh_encode_workspace_bytes(width, height))
+        self.workspace = torch.empty(ws + 256, dtype=torch.uint8, device=self.device)
+        self.cap = (self.nb * 64 * 2 + N.MH_CODES_PAD + 3) // 4 * 4 + 16
+
+    def encode(self, gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False,
+               stream: Optional[torch.cuda.Stream] = None) -> DeviceEncodedFrame:
+        if gray.dtype != torch.uint8 or gray.shape != (self.height, self.width) or not gray.is_contiguous():
+            raise ValueError(f"gray must be contiguous uint8 [{self.height}, {self.width}]")
+        gray = gray.to(self.device)
+        codes = torch.empty(self.cap, dtype=torch.uint8, device=self.device)
+        offs = torch.empty(self.nb, dtype=torch.int32, device=self.device)
+        init = torch.empty(self.nb, dtype=torch.uint8, device=self.device) if init_zero_delta else None
+        canon = np.zeros(256, np.uint8)
+        n = ctypes.c_uint64(0)
+        base = self.workspace.data_ptr()
+        aligned = (base + 255) // 256 * 256
+        N.check(N.lib().mh_encode_frame_device(
+            gray.data_ptr(), self.width, self.height, flags,
+            canon.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), codes.data_ptr(), self.cap,
+            ctypes.byref(n), offs.data_ptr(), init.data_ptr() if init is not None else None,
+            aligned, self.workspace.numel() - (aligned - base), _stream_ptr(stream, self.device)),
+            "mh_encode_frame_device")
+        return DeviceEncodedFrame(self.width, self.height, canon, codes[: n.value], offs, init, flags)
+
+
+def encode_frame_device(gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False) -> DeviceEncodedFrame:
+    """One-shot GPU encode of a [H, W] uint8 device tensor."""
+    h, w = gray.shape
+    return Encoder(w, h, gray.device).encode(gray, flags, init_zero_delta)

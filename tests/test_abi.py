@@ -99,6 +99,17 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_stream_create(ctypes.byref(_frame(dims=N.mh_dims(16, 16, 3, 2))), 4096, 2, None,
                               ctypes.byref(h)) == -2
     assert L.mh_stream_submit(None, 0x1000, 4096, 0x2000, None, None) == -1
+    n = ctypes.c_uint64()
+    canon = (ctypes.c_uint8 * 256)()
+    assert L.mh_encode_frame_device(None, 8, 8, 0, canon, 0x1000, 64, ctypes.byref(n), 0x2000, None,
+                                    0x10000, 1 << 20, None) == -1
+    assert L.mh_encode_frame_device(0x100, 0, 8, 0, canon, 0x1000, 64, ctypes.byref(n), 0x2000, None,
+                                    0x10000, 1 << 20, None) == -2
+    assert L.mh_encode_frame_device(0x100, 8, 8, 0, canon, 0x1002, 64, ctypes.byref(n), 0x2000, None,
+                                    0x10000, 1 << 20, None) == -6
+    assert L.mh_encode_frame_device(0x100, 8, 8, 0, canon, 0x1000, 64, ctypes.byref(n), 0x2000, None,
+                                    0x10000, 16, None) == -4
+    assert L.mh_encode_workspace_bytes(2048, 1536) >= 49152 * 64
 
 
 def test_constants(mh):
