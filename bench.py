@@ -225,6 +225,32 @@ def stream_h2d(efs, tables, device, n_frames=2048, warmup=1024):
             "slots": 2, "launch": "native mh_stream: one H2D DMA per frame on a copy stream + per-slot hipGraph decode"}
 
 
+def encode_rate(device, bb, reps=32):
+    """The producer side: GPU encoder (mh_encode_frame_device: one host sync for the
+    histogram per frame) vs the host codec (mh_encode_frame, one thread), both on
+    BigBridge-shuffled frames, wall clock per frame."""
+    import metalhuffman_amd as mh
+    from metalhuffman_amd import frames as F
+    from metalhuffman_amd.encoder import Encoder
+    imgs = [F.block_shuffle(bb, 900 + k) for k in range(4)]
+    dimgs = [torch.from_numpy(im).to(device) for im in imgs]
+    enc = Encoder(bb.shape[1], bb.shape[0], device)
+    for k in range(4):
+        enc.encode(dimgs[k])
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        enc.encode(dimgs[k % 4])
+    torch.cuda.synchronize(device)
+    gpu_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for k in range(4):
+        mh.encode_frame(imgs[k])
+    cpu_s = (time.perf_counter() - t0) / 4
+    return {"gpu_ms_per_frame": round(gpu_s * 1e3, 3), "gpu_MBps": round(bb.size / gpu_s / 1e6, 1),
+            "host_1thread_ms_per_frame": round(cpu_s * 1e3, 2), "host_1thread_MBps": round(bb.size / cpu_s / 1e6, 1)}
+
+
 def cpu_baseline(efs, threads):
     """The reference's CPU decode (HuffmanUtil::decodeHuffmanBitsFromTables,
     Shared/HuffmanUtil.cpp:830-1046) restated in oracle/ (kind 'port'), timed on
@@ -383,6 +409,7 @@ def main(argv=None) -> int:
                             "roofline": roofline(w2.bytes, reg2, steps, kms2, key)}
             del w2
         extras["stream_h2d"] = stream_h2d(efs, tables, dev)  # config 5, one GPU
+        extras["encode"] = encode_rate(dev, bb)
         result["extras"] = extras
 
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

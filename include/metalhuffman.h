@@ -247,6 +247,15 @@ int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]);
 int mh_build_tables(const uint8_t canon_header[256], mh_lookup_symbol table1[256],
                     mh_lookup_symbol *table2, uint32_t table2_cap, uint32_t *table2_entries);
 
+/* The 8-byte container header HuffmanEncoder::encode emits ahead of the
+ * canonical table (HuffmanEncoder.cpp:326-340: u32 LE 0xFFEEEEDD, u32 LE symbol
+ * count) and HuffmanUtil::encodeHuffman drops (HuffmanUtil.cpp:1073-1086). */
+#define MH_CONTAINER_HEADER_BYTES 8
+#define MH_CONTAINER_MAGIC 0xFFEEEEDDu
+int mh_container_header(uint64_t n_symbols, uint8_t header[MH_CONTAINER_HEADER_BYTES]);
+/* MH_ERR_INVALID_ARG when the magic word does not match. */
+int mh_parse_container_header(const uint8_t header[MH_CONTAINER_HEADER_BYTES], uint64_t *n_symbols);
+
 /* Huffman code lengths (the canonical header) from 256 symbol counts, with the
  * reference tree's tie-breaking (HuffmanEncoder.cpp:29-145). MH_ERR_EMPTY for no
  * symbols, MH_ERR_CODE_TOO_LONG past 16 bits (lengths still written). */

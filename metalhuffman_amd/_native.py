@@ -26,6 +26,7 @@ EXPORTS = (
     "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
     "mh_stream_compute_stream", "mh_stream_wait", "mh_stream_synchronize", "mh_stream_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
+    "mh_container_header", "mh_parse_container_header",
 )
 
 
@@ -91,6 +92,8 @@ def lib() -> ctypes.CDLL:
         L.mh_stream_synchronize.argtypes = [_vp]
         L.mh_stream_destroy.argtypes = [_vp]
         L.mh_code_lengths.argtypes = [_u64p, _u8p]
+        L.mh_container_header.argtypes = [ctypes.c_uint64, _u8p]
+        L.mh_parse_container_header.argtypes = [_u8p, _u64p]
         L.mh_encode_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.mh_encode_workspace_bytes.restype = ctypes.c_size_t
         L.mh_encode_frame_device.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

@@ -138,6 +138,24 @@ class Huffman:
         return (np.zeros(0, np.uint8), canon, codes[: ln.value].copy(),
                 offs[: sym.size // stride].copy())
 
+    @staticmethod
+    def containerHeader(n_symbols: int) -> np.ndarray:
+        """The 8-byte header HuffmanEncoder::encode emits (HuffmanEncoder.cpp:326-340)
+        and encodeHuffman drops: u32 LE 0xFFEEEEDD, u32 LE symbol count."""
+        out = np.zeros(8, np.uint8)
+        N.check(N.lib().mh_container_header(int(n_symbols), _p(out)), "containerHeader")
+        return out
+
+    @staticmethod
+    def parseContainerHeader(header) -> int:
+        """Symbol count of a container header (MHError on a wrong magic word)."""
+        h = _u8(header)
+        if h.size != 8:
+            raise N.MHError(-1, "parseContainerHeader")
+        n = ctypes.c_uint64(0)
+        N.check(N.lib().mh_parse_container_header(_p(h), ctypes.byref(n)), "parseContainerHeader")
+        return int(n.value)
+
     # +encodeSignedByteDeltas: / +decodeSignedByteDeltas: (Huffman.h:72-76)
     @staticmethod
     def encodeSignedByteDeltas(data) -> np.ndarray:

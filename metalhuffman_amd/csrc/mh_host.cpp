@@ -255,6 +255,25 @@ int mh_encode_frame(const uint8_t *gray, uint32_t width, uint32_t height, uint32
   return MH_OK;
 }
 
+int mh_container_header(uint64_t n_symbols, uint8_t header[MH_CONTAINER_HEADER_BYTES]) {
+  if (!header) return MH_ERR_INVALID_ARG;
+  if (n_symbols > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
+  const uint32_t words[2] = {MH_CONTAINER_MAGIC, (uint32_t)n_symbols};
+  for (int w = 0; w < 2; ++w)
+    for (int k = 0; k < 4; ++k) header[4 * w + k] = (uint8_t)(words[w] >> (8 * k));
+  return MH_OK;
+}
+
+int mh_parse_container_header(const uint8_t header[MH_CONTAINER_HEADER_BYTES], uint64_t *n_symbols) {
+  if (!header || !n_symbols) return MH_ERR_INVALID_ARG;
+  uint32_t words[2] = {0, 0};
+  for (int w = 0; w < 2; ++w)
+    for (int k = 0; k < 4; ++k) words[w] |= (uint32_t)header[4 * w + k] << (8 * k);
+  if (words[0] != MH_CONTAINER_MAGIC) return MH_ERR_INVALID_ARG;
+  *n_symbols = words[1];
+  return MH_OK;
+}
+
 int mh_code_lengths(const uint64_t freq[256], uint8_t canon_header[256]) {
   if (!freq || !canon_header) return MH_ERR_INVALID_ARG;
   return code_lengths(freq, canon_header);

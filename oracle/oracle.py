@@ -204,8 +204,9 @@ def time_decode_frames(t1, t2, nsym: int, bufs: list, n_threads: int, reps: int 
     return lib().orc_time_decode_frames(_p(t1), _p(t2), nsym, b_arr, o_arr, n, n_threads, reps)
 
 
-def ref_encode(sym: np.ndarray, stride: int = 64):
-    """Run the REAL reference encoder (oracle/_ref/ref_encode). Container only."""
+def ref_encode(sym: np.ndarray, stride: int = 64, with_header: bool = False):
+    """Run the REAL reference encoder (oracle/_ref/ref_encode). Container only.
+    -> canon, codes, offsets (+ the 8-byte container header with with_header)."""
     if not os.path.exists(REF_ENCODE):
         raise FileNotFoundError(REF_ENCODE)
     with tempfile.TemporaryDirectory() as d:
@@ -217,4 +218,5 @@ def ref_encode(sym: np.ndarray, stride: int = 64):
         canon = np.fromfile(pre + ".canon", np.uint8)
         codes = np.fromfile(pre + ".codes", np.uint8)
         offs = np.fromfile(pre + ".offsets", np.uint32)
-    return canon, codes, offs
+        header = np.fromfile(pre + ".header", np.uint8)
+    return (canon, codes, offs, header) if with_header else (canon, codes, offs)

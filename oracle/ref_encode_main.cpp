@@ -10,7 +10,8 @@
 //
 // usage: ref_encode <symbols.bin> <stride> <out_prefix>
 //   writes <out_prefix>.canon (256 B), .codes (encoder bytes incl. its 2 zero
-//   bytes) and .offsets (u32 little-endian, one per stride symbols).
+//   bytes), .offsets (u32 little-endian, one per stride symbols) and .header
+//   (the 8-byte container header encode() emits and the renderer drops).
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -53,5 +54,6 @@ int main(int argc, char **argv) {
   if (!write_file(p + ".canon", canon.data(), canon.size())) return 6;
   if (!write_file(p + ".codes", codes.data(), codes.size())) return 6;
   if (!write_file(p + ".offsets", offsets.data(), offsets.size() * sizeof(uint32_t))) return 6;
+  if (!write_file(p + ".header", header.data(), header.size())) return 6;
   return 0;
 }

@@ -126,11 +126,12 @@ def main() -> int:
     for name, (w, h, px) in SMALL.items():
         img = np.array(px, np.uint8).reshape(h, w)
         sym = producer_symbols(img)
-        canon, codes, offs = O.ref_encode(sym, 64)
+        canon, codes, offs, header = O.ref_encode(sym, 64, with_header=True)
         out["small_frames"][name] = {
             "width": w, "height": h, "pixels": px,
             "canon": {str(i): int(c) for i, c in enumerate(canon) if c},
             "codes_hex": codes.tobytes().hex(), "block_offsets": offs.tolist(),
+            "container_header_hex": header.tobytes().hex(),
         }
     img6 = np.array(SMALL["TEST_6x4_NOT_SQUARE"][2], np.uint8).reshape(4, 6)
     sym6 = producer_symbols(img6, block_dim=2, delta=False)

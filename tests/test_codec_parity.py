@@ -96,3 +96,16 @@ def test_errors(mh):
     with pytest.raises(MHError) as e:
         mh.encode_frame(np.zeros((1, 70000), np.uint8))
     assert e.value.status == -2   # MH_ERR_DIMS: beyond the u16 dims uniform
+
+
+def test_container_header_matches_reference_encoder(mh):
+    """HuffmanEncoder::encode's 8-byte header (golden.json, emitted by the real
+    reference encoder for every hand-written frame)."""
+    from helpers import golden
+    for name, fx in golden()["small_frames"].items():
+        n = -(-fx["width"] // 8) * -(-fx["height"] // 8) * 64      # symbols after the 8x8 split
+        hdr = mh.Huffman.containerHeader(n)
+        assert hdr.tobytes().hex() == fx["container_header_hex"], name
+        assert mh.Huffman.parseContainerHeader(hdr) == n
+    with pytest.raises(mh.MHError):
+        mh.Huffman.parseContainerHeader(bytes(8))
