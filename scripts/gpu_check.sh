@@ -1,4 +1,5 @@
-# GPU round check: parity tests, smoke, bench, rocprofv3 kernel trace (fail-fast).
+# GPU round check: parity tests, smoke, bench, then rocprofv3 kernel traces of the
+# bench command per workload (fail-fast).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -9,6 +10,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 echo "smoke ok"
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
-rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || { tail gpurun_out/bench_prof.err; exit 1; }
-python3 scripts/ktrace_summary.py gpurun_out/prof > gpurun_out/ktrace_summary.txt && cat gpurun_out/ktrace_summary.txt
+: > gpurun_out/ktrace_summary.txt
+for wl in frame batch tile8192; do
+  rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_$wl
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }
+  { echo "== bench.py --workload $wl (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl; } >> gpurun_out/ktrace_summary.txt
+done
+cat gpurun_out/ktrace_summary.txt
