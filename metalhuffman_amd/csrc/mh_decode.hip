@@ -49,6 +49,9 @@ namespace {
 #ifndef MH_PRIO_ROTATE          // wave priority: 0 off, 1 rotate per tile, 2 per block row,
 #define MH_PRIO_ROTATE 3        // 3 by remaining tiles (default)
 #endif
+#ifndef MH_PERM3                // 1: assemble output words from 4 lane states (3 VALU / 4 bytes)
+#define MH_PERM3 1
+#endif
 #ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
 #define MH_SMALL_KERNEL 1
 #endif
@@ -199,6 +202,13 @@ __device__ __forceinline__ uint32_t word_at(const uint8_t *q) {
   return *reinterpret_cast<const uint32_t *>(q);
 }
 
+// byte 1 (prev) of four successive lane states -> one output word, 3 VALU
+__device__ __forceinline__ uint32_t pack_prev4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0501u);  // [a.1, b.1, 0, 0]
+  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x05010C0Cu);  // [0, 0, c.1, d.1]
+  return lo | hi;
+}
+
 // v_perm_b32 selectors: put S0.byte1 at byte J, keep S1's other bytes
 __device__ __forceinline__ constexpr uint32_t ins_sel1(int j) {
   return j == 0 ? 0x03020105u : j == 1 ? 0x03020500u : j == 2 ? 0x03050100u : 0x05020100u;
@@ -286,7 +296,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     }                                                                               \
     S += e;                                                                         \
     if (kDelta) {                                                                   \
-      OW = __builtin_amdgcn_perm(S, OW, ins_sel1(J));                               \
+      if (MH_PERM3) sv[J] = S; else OW = __builtin_amdgcn_perm(S, OW, ins_sel1(J));  \
     } else {                                                                        \
       OW = __builtin_amdgcn_perm(e + 0x100u, OW, ins_sel1(J));                      \
     }                                                                               \
@@ -332,6 +342,8 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     set_prio(prio + r);
 #endif
     uint32_t o0 = 0, o1 = 0;
+    uint32_t sv[4];  // MH_PERM3: S after each symbol of the current output word
+    (void)sv;
     if (r) {
       MH_STEP_R(0, o0);
     } else {
@@ -340,10 +352,12 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     MH_STEP(1, o0);
     MH_STEP_R(2, o0);
     MH_STEP(3, o0);
+    if (MH_PERM3 && kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
     MH_STEP_R(0, o1);
     MH_STEP(1, o1);
     MH_STEP_R(2, o1);
     MH_STEP(3, o1);
+    if (MH_PERM3 && kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
     // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
     // block and rows below the frame use offsets outside the descriptor's range,
     // which the hardware drops. A right-edge block writes its 8 bytes into the
