@@ -94,7 +94,7 @@ struct DecodeArgs {
   uint8_t *out;
   uint64_t out_pitch;
   uint64_t out_frame_stride;
-  uint32_t out_frame_bytes;    // H * pitch (< 2^32): range of the per-frame store descriptor
+  uint64_t out_frame_bytes;    // H * pitch
   uint32_t t2_entries;
   uint32_t w, h, bw, bh, nb;
   uint32_t tiles_per_frame, total_tiles;
@@ -482,6 +482,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t codes_rsrc(const DecodeArgs &a
   return uniform_rsrc(a.codes + t.fbeg, t.fb32);
 }
 
+// Output addressing of a tile: a store descriptor based at the tile's first block
+// row (64-bit base, so frames beyond 4 GB of raster work) and each lane's offset
+// of its block's first row from there. Stores below row H fall outside the
+// descriptor's range and are dropped.
+struct OutTile {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t row0;
+};
+__device__ __forceinline__ OutTile out_tile(const DecodeArgs &a, const Tile &t, uint32_t lane) {
+  const uint32_t b = t.b0 + lane;
+  const uint32_t bx = b % a.bw, by = b / a.bw;
+  const uint32_t by0 = __builtin_amdgcn_readfirstlane(t.b0 / a.bw);
+  const uint64_t base = (uint64_t)by0 * 8u * a.out_pitch;
+  const uint64_t rem = a.out_frame_bytes > base ? a.out_frame_bytes - base : 0u;
+  OutTile o;
+  o.rsrc = uniform_rsrc(a.out + (uint64_t)t.f * a.out_frame_stride + base,
+                        (uint32_t)(rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull));
+  o.row0 = (by - by0) * 8u * (uint32_t)a.out_pitch + bx * 8u;
+  return o;
+}
+
 __device__ __forceinline__ void span_issue(const DecodeArgs &a, const Tile &t, uint32_t lane,
                                            v4u32 (&R)[kStageChunks], bool on = true) {
   // Unconditional loads (no exec-masked branches, so the compiler can count them
@@ -629,12 +650,10 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 
     wave_sync();  // this tile's staging writes -> reads
     {
-      const uint32_t b = cur.b0 + lane;
-      const uint32_t bx = b % a.bw, by = b / a.bw;
       const bool dead = !cur.valid;
-      const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
-      const __amdgpu_buffer_rsrc_t out =
-          uniform_rsrc(a.out + (uint64_t)cur.f * a.out_frame_stride, a.out_frame_bytes);
+      const OutTile ot = out_tile(a, cur, lane);
+      const __amdgpu_buffer_rsrc_t out = ot.rsrc;
+      const uint32_t row0 = ot.row0;
       LdsWords src{stage};
 #if MH_PRIO_ROTATE == 1
       set_prio(prio);
@@ -666,12 +685,8 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     TileHdr h;
     hdr_issue(a, t, lane, h);
     const Tile tt = hdr_resolve(a, h, lane);
-    const uint32_t b = tt.b0 + lane;
-    const uint32_t bx = b % a.bw, by = b / a.bw;
-    const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
-    const __amdgpu_buffer_rsrc_t out =
-        uniform_rsrc(a.out + (uint64_t)tt.f * a.out_frame_stride, a.out_frame_bytes);
-    decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, out, row0, !tt.valid);
+    const OutTile ot = out_tile(a, tt, lane);
+    decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
   }
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
@@ -721,11 +736,9 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves) mh_decode_small_kernel(co
   span_issue(a, t, lane, R, staged);
   __syncthreads();  // table in LDS
   if (!live) return;  // no barrier below
-  const uint32_t b = t.b0 + lane;
-  const uint32_t bx = b % a.bw, by = b / a.bw;
-  const uint32_t row0 = by * 8u * (uint32_t)a.out_pitch + bx * 8u;
-  const __amdgpu_buffer_rsrc_t out =
-      uniform_rsrc(a.out + (uint64_t)t.f * a.out_frame_stride, a.out_frame_bytes);
+  const OutTile ot = out_tile(a, t, lane);
+  const __amdgpu_buffer_rsrc_t out = ot.rsrc;
+  const uint32_t row0 = ot.row0;
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
@@ -845,10 +858,10 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (((uintptr_t)fr->d_codes & 15u) || (out_pitch & 7u) || ((uintptr_t)d_out & 7u) ||
       (fr->n_frames > 1 && (out_frame_stride & 7u)) || ((uintptr_t)fr->d_lut & 15u))
     return MH_ERR_ALIGN;
-  if (out_pitch < d.width || (fr->n_frames > 1 && out_frame_stride < out_pitch * d.height))
+  if (out_pitch < d.width || out_pitch > (1u << 20) ||
+      (fr->n_frames > 1 && out_frame_stride < out_pitch * d.height))
     return MH_ERR_CAPACITY;
   if (fr->codes_bytes < MH_CODES_PAD) return MH_ERR_CAPACITY;
-  if ((uint64_t)d.height * out_pitch > 0x7FFFFFF0ull) return MH_ERR_CAPACITY;  // store descriptor range
   if (fr->n_frames == 1 && !fr->d_frame_code_offsets && fr->codes_bytes > 0xFFFFFFF0ull)
     return MH_ERR_CAPACITY;
 
@@ -864,7 +877,7 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   a.out = d_out;
   a.out_pitch = out_pitch;
   a.out_frame_stride = out_frame_stride;
-  a.out_frame_bytes = (uint32_t)((uint64_t)d.height * out_pitch);
+  a.out_frame_bytes = (uint64_t)d.height * out_pitch;
   a.t2_entries = fr->table2_entries;
   a.w = d.width;
   a.h = d.height;

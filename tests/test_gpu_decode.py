@@ -189,3 +189,23 @@ def test_garbage_stream_no_fault(mh, device, bigbridge):
     ef.codes = bad
     out = _decode([ef], device)[0]
     assert out.shape == (768, 1024)
+
+
+def test_raster_beyond_2_gib(mh, device):
+    """Maximum-size corner: a 65535-wide frame whose raster exceeds 2 GiB (and the
+    u32 store range of one descriptor). Encoded and checked on the device only."""
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd.encoder import encode_frame_device
+    W, H = 65535, 32800
+    y = torch.arange(H, device=device, dtype=torch.int32).view(H, 1) // 8
+    x = torch.arange(W, device=device, dtype=torch.int32).view(1, W) // 8
+    img = ((x * 7 + y * 3) & 0xFF).to(torch.uint8).contiguous()  # one value per 8x8 block
+    assert img.numel() > 2 ** 31
+    ef = encode_frame_device(img)
+    t1, t2 = mh.Huffman.generateSplitLookupTables(ef.canon)
+    out = D.decode(ef.frames(), D.DeviceTables.upload(t1, t2, device))
+    torch.cuda.synchronize(device)
+    assert torch.equal(out[0, :, :W], img)
+    del out, ef, img
+    torch.cuda.empty_cache()
