@@ -705,36 +705,56 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 // throughput) sets the time: the step takes the refill off the chain (kSpec), and
 // when the table has no code longer than 14 bits the single-level 14-bit table
 // drops the escape test from it too.
-constexpr int kSmallMaxWaves = 4;
+constexpr int kSmallWaves = 8;           // waves per workgroup (one tile each)
+constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
 
 template <bool kDelta>
-__global__ void __launch_bounds__(64 * kSmallMaxWaves) mh_decode_small_kernel(const DecodeArgs a) {
+__global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = blockDim.x >> 6;
   uint8_t *stage = s_stage + wave * kStageBytes;
   const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut_small);
   const uint8_t *prepared = reinterpret_cast<const uint8_t *>(a.lut);
+#if MH_DIAG_STAMPS
+  unsigned long long ts[kDiagSlots] = {};
+#endif
+  MH_STAMP(0);
 
   const uint32_t max_len = *reinterpret_cast<const uint32_t *>(prepared + kMaxLenOff);  // scalar load
   const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr h;
   hdr_issue(a, tile, lane, h);
   const bool l14 = max_len <= (uint32_t)kLut14Bits;
+  // Table copy: a fixed count of unconditional 16-B loads per thread (chunks past
+  // the table fall outside the descriptor), issued behind the offsets so that the
+  // offsets wait below is an exact vmcnt leaving the table loads in flight; the
+  // table's L2 round trip overlaps the offsets' HBM one.
+  constexpr int kLutLoads = kLut14Bytes / 16 / (64 * kSmallWaves);  // 4
+  static_assert(kLut14Bytes == kLutLoads * 16 * 64 * kSmallWaves, "whole table per pass");
+  v4u32 L[kLutLoads];
   {
-    const v4u32 *src = reinterpret_cast<const v4u32 *>(prepared + (l14 ? kLut14Off : 0));
-    v4u32 *dst = reinterpret_cast<v4u32 *>(s_lut_small);
-    const uint32_t n16 = (uint32_t)(l14 ? kLut14Bytes : kLutBytes) / 16u;
-    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    const __amdgpu_buffer_rsrc_t rl =
+        uniform_rsrc(prepared + (l14 ? kLut14Off : 0), l14 ? (uint32_t)kLut14Bytes : (uint32_t)kLutBytes);
+#pragma unroll
+    for (int k = 0; k < kLutLoads; ++k)
+      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + 64u * kSmallWaves * k) * 16u), 0, 0);
   }
   const Tile t = hdr_resolve(a, h, lane);
+  MH_STAMP(1);
   const bool live = t.tile < a.total_tiles;
   const bool staged = live && t.span <= (uint32_t)kStageBytes;
   v4u32 R[kStageChunks];
   span_issue(a, t, lane, R, staged);
+  {
+    v4u32 *dst = reinterpret_cast<v4u32 *>(s_lut_small);
+#pragma unroll
+    for (int k = 0; k < kLutLoads; ++k) dst[threadIdx.x + 64u * kSmallWaves * k] = L[k];
+  }
   __syncthreads();  // table in LDS
+  MH_STAMP(2);
   if (!live) return;  // no barrier below
   const OutTile ot = out_tile(a, t, lane);
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
@@ -742,6 +762,7 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves) mh_decode_small_kernel(co
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
+    MH_STAMP(3);
     LdsWords src{stage};
     if (l14)
       decode_block<kDelta, StepCfg<kLut14Bits, true>>(src, lut, t.p, t.init, out, row0,
@@ -754,6 +775,17 @@ __global__ void __launch_bounds__(64 * kSmallMaxWaves) mh_decode_small_kernel(co
   } else {
     decode_halves<kDelta, StepCfg<kLutBits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
+#if MH_DIAG_STAMPS
+  MH_STAMP(4);
+  ts[5] = ts[4];
+  __builtin_amdgcn_s_waitcnt(0);
+  MH_STAMP(6);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+  ts[7] = ((unsigned long long)xcc << 48) | ((unsigned long long)__smid() << 32) | blockIdx.x;
+  const uint32_t gw = blockIdx.x * nwaves + wave;
+  if (lane == 0 && gw < (uint32_t)kDiagWaves)
+    for (int i = 0; i < kDiagSlots; ++i) g_stamps[gw * kDiagSlots + i] = ts[i];
+#endif
 }
 
 int g_cu_count = 0;
@@ -789,9 +821,10 @@ int launch(const DecodeArgs &a0, hipStream_t s) {
   DecodeArgs a = a0;
   const int cus = cu_count();
   if (!cus) return MH_ERR_HIP;
-  if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxWaves * cus)) {
-    // one tile per wave, at most kSmallMaxWaves waves per CU
-    const uint32_t nw = (a.total_tiles + (uint32_t)cus - 1) / (uint32_t)cus;
+  if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
+    // one tile per wave, kSmallWaves waves per workgroup: fewer workgroups copy the
+    // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
+    const uint32_t nw = kSmallWaves;
     a.n_groups = (a.total_tiles + nw - 1) / nw;
     hipLaunchKernelGGL(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), 0, s, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
