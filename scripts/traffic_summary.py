@@ -1,4 +1,5 @@
-"""Per-launch HBM bytes of mh_decode_kernel from rocprofv3 --pmc CSVs (gpu_traffic.sh).
+"""Per-launch HBM bytes of the decode kernels (mh_decode_kernel, mh_decode_small_kernel)
+from rocprofv3 --pmc CSVs (gpu_traffic.sh).
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are in
 KiB; FETCH_SIZE reports half the bytes of wide coalesced streaming reads (x2);
@@ -13,13 +14,16 @@ import sys
 
 root = sys.argv[1]
 res = {}
+kernels = {}
 for d in sorted(glob.glob(os.path.join(root, "*_*_SIZE"))):
     wl, ctr = os.path.basename(d).split("_", 1)
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "mh_decode_kernel" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+            kn = r["Kernel_Name"]
+            if ("mh_decode_kernel" in kn or "mh_decode_small_kernel" in kn) and r["Counter_Name"] == ctr:
                 vals.append(float(r["Counter_Value"]))
+                kernels[wl] = "mh_decode_small_kernel" if "small" in kn else "mh_decode_kernel"
     if vals:
         res.setdefault(wl, {})[ctr] = statistics.median(vals) * 1024.0
         res[wl]["dispatches"] = len(vals)
@@ -28,7 +32,7 @@ for wl, v in res.items():
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         out[wl] = {"fetch_bytes_x2": round(2 * v["FETCH_SIZE"]), "write_bytes": round(v["WRITE_SIZE"]),
                    "traffic_bytes": round(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]),
-                   "dispatches": v["dispatches"]}
-print(json.dumps({"kernel": "mh_decode_kernel", "per_launch_median": out,
+                   "dispatches": v["dispatches"], "kernel": kernels[wl]}
+print(json.dumps({"per_launch_median": out,
                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950)"},
                  indent=1))
