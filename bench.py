@@ -49,7 +49,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["frame", "batch", "tile8192"], default="frame")
+    ap.add_argument("--workload", choices=["frame", "batch", "tile8192", "tile8192_random"], default="frame")
     ap.add_argument("--frames", type=int, default=64, help="distinct resident frames per rank")
     ap.add_argument("--batch", type=int, default=64, help="frames per launch for --workload batch")
     ap.add_argument("--no-extras", action="store_true", help="skip the batch/tile side measurements")
@@ -225,6 +225,28 @@ def stream_h2d(efs, tables, device, n_frames=2048, warmup=1024):
             "slots": 2, "launch": "native mh_stream: one H2D DMA per frame on a copy stream + per-slot hipGraph decode"}
 
 
+def copy_bandwidth(device, nbytes=1 << 30, reps=20):
+    """Achievable HBM bandwidth on this box: a device-to-device copy of 1 GiB
+    (read + write bytes / time, best of `reps`), reported beside the spec peak
+    (SURVEY.md 8(d))."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(device)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize(device)
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return {"bytes_moved": 2 * nbytes, "best_ms": round(best, 4),
+            "GBps": round(2 * nbytes / (best * 1e-3) / 1e9, 1), "kernel": "torch copy_ (D2D)"}
+
+
 def encode_rate(device, bb, reps=32):
     """The producer side: GPU encoder (mh_encode_frame_device: one host sync for the
     histogram per frame) vs the host codec (mh_encode_frame, one thread), both on
@@ -344,14 +366,17 @@ def main(argv=None) -> int:
         launches = [pack(g) for g in groups]
         return Workload(f"batch{nb}", launches, tables, nb * bb.size, algo_bytes(groups[0], t2_bytes), dev)
 
-    def tile_workload():
-        base = F.mirror_tile(bb, 8192, 8192)
+    def tile_workload(random=False):
+        # config 3: BigBridge mirror tile (primary) or uniform random bytes (stress:
+        # 8 bits/symbol, every code 8 bits, no T2 subtable), SURVEY.md 8(d)
+        base = F.uniform_random(8192, 8192, 1234) if random else F.mirror_tile(bb, 8192, 8192)
         imgs = [base] + [F.block_shuffle(base, 100 + k) for k in range(2)]
         tefs = encode_many(imgs, threads=3)
         t1t, t2t = tefs[0].tables()
         ttabs = D.DeviceTables.upload(t1t, t2t, dev)
         launches = [pack([ef]) for ef in tefs]
-        return Workload("tile8192", launches, ttabs, base.size, algo_bytes(tefs[:1], ttabs.table2.numel()), dev)
+        name = "tile8192_random" if random else "tile8192"
+        return Workload(name, launches, ttabs, base.size, algo_bytes(tefs[:1], ttabs.table2.numel()), dev)
 
     if args.workload == "frame":
         wl = frame_workload()
@@ -359,15 +384,20 @@ def main(argv=None) -> int:
     elif args.workload == "batch":
         wl = batch_workload(args.batch)
         wdesc = f"config4 shard: {args.batch} 2048x1536 frames per launch per GPU"
-    else:
+    elif args.workload == "tile8192":
         wl = tile_workload()
         wdesc = "config3: one 8192x8192 BigBridge mirror-tile per launch per GPU"
+    else:
+        wl = tile_workload(random=True)
+        wdesc = "config3 stress: one 8192x8192 uniform-random frame per launch per GPU"
 
     # parity guard: the timed path must produce the exact frames
     wl.launch(0)
     torch.cuda.synchronize(dev)
     chk = wl.outs[0][0, :, : wl.launches[0].width].cpu().numpy()
-    ref_img = F.block_shuffle(bb, seeds[0]) if args.workload != "tile8192" else F.mirror_tile(bb, 8192, 8192)
+    ref_img = {"tile8192": lambda: F.mirror_tile(bb, 8192, 8192),
+               "tile8192_random": lambda: F.uniform_random(8192, 8192, 1234)}.get(
+        args.workload, lambda: F.block_shuffle(bb, seeds[0]))()
     if not np.array_equal(chk, ref_img) and not os.environ.get("MH_LIB"):
         raise SystemExit("bench: decoded frame differs from the encoder input")
 
@@ -396,10 +426,12 @@ def main(argv=None) -> int:
         extras = {}
         # ~20 ms of launches each, after a warm-up of the same length (clocks settle)
         for name, make, steps, key in (("batch64", lambda: batch_workload(args.batch), 256, "batch"),
-                                       ("tile8192", tile_workload, 512, "tile8192")):
+                                       ("tile8192", tile_workload, 512, "tile8192"),
+                                       ("tile8192_random", lambda: tile_workload(True), 512,
+                                        "tile8192_random")):
             if name.startswith("batch") and args.workload == "batch":
                 continue
-            if name == "tile8192" and args.workload == "tile8192":
+            if name == args.workload:
                 continue
             w2 = make()
             wall2, reg2, kms2 = w2.run(steps, steps, use_graph=not args.no_graph)
@@ -408,6 +440,7 @@ def main(argv=None) -> int:
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
                             "roofline": roofline(w2.bytes, reg2, steps, kms2, key)}
             del w2
+        extras["hbm_copy"] = copy_bandwidth(dev)  # achievable HBM rate beside the 8 TB/s spec
         extras["stream_h2d"] = stream_h2d(efs, tables, dev)  # config 5, one GPU
         extras["encode"] = encode_rate(dev, bb)
         result["extras"] = extras

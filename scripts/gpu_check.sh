@@ -11,7 +11,7 @@ echo "smoke ok"
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 : > gpurun_out/ktrace_summary.txt
-for wl in frame batch tile8192; do
+for wl in frame batch tile8192 tile8192_random; do
   rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_$wl
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }
   { echo "== bench.py --workload $wl (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl; } >> gpurun_out/ktrace_summary.txt

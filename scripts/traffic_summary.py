@@ -16,7 +16,9 @@ root = sys.argv[1]
 res = {}
 kernels = {}
 for d in sorted(glob.glob(os.path.join(root, "*_*_SIZE"))):
-    wl, ctr = os.path.basename(d).split("_", 1)
+    base = os.path.basename(d)
+    ctr = "FETCH_SIZE" if base.endswith("FETCH_SIZE") else "WRITE_SIZE"
+    wl = base[: -len(ctr) - 1]
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):

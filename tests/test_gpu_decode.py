@@ -209,3 +209,51 @@ def test_raster_beyond_2_gib(mh, device):
     assert torch.equal(out[0, :, :W], img)
     del out, ef, img
     torch.cuda.empty_cache()
+
+
+def test_small_launch_multi_frame(mh, oracle, device, bigbridge):
+    """A few frames in one launch (frame code offsets) take the one-tile-per-wave
+    kernel: 3 x 192 tiles, 14-bit table."""
+    from metalhuffman_amd import frames as F
+    base = np.ascontiguousarray(bigbridge[:1024, :768])
+    imgs = [F.block_shuffle(base, s) if s else base for s in range(3)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    assert efs[0].canon.max() <= 14
+    out = _decode(efs, device)
+    for i, (im, ef) in enumerate(zip(imgs, efs)):
+        assert np.array_equal(out[i], im), i
+        assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
+
+
+@pytest.mark.parametrize("mode", ["long_codes", "no_delta", "init_zero_delta"])
+def test_small_launch_multi_frame_variants(mh, oracle, device, bigbridge, mode):
+    """Multi-frame small launches with the 13-bit table (16-bit codes), raw symbols,
+    and per-block init bytes."""
+    from metalhuffman_amd import frames as F
+    if mode == "long_codes":
+        d = fibonacci_deltas(17, 256 * 256, seed=11)
+        base = image_from_block_deltas(d, 256, 256)
+        kw = {}
+    elif mode == "no_delta":
+        base = fibonacci_deltas(17, 256 * 256, seed=12).reshape(256, 256)
+        kw = {"flags": mh.MH_FLAG_NO_DELTA}
+    else:
+        base = np.ascontiguousarray(bigbridge[:768, :1024])
+        kw = {"init_zero_delta": True}
+    imgs = [F.block_shuffle(base, 40 + s) for s in range(3)]
+    efs = [mh.encode_frame(im, **kw) for im in imgs]
+    out = _decode(efs, device)
+    for i, (im, ef) in enumerate(zip(imgs, efs)):
+        assert np.array_equal(out[i], im), i
+        assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
+
+
+@pytest.mark.parametrize("h", [2048, 2056])
+def test_small_batch_kernel_boundary(mh, device, bigbridge, h):
+    """2048x2048 = 1024 tiles (the small kernel's limit on a 256-CU part) and
+    2048x2056 = 1028 tiles (the batch kernel): same bytes either side."""
+    from metalhuffman_amd import frames as F
+    img = F.mirror_tile(bigbridge, h, 2048)
+    ef = mh.encode_frame(img)
+    out = _decode([ef], device)[0]
+    assert np.array_equal(out, img)
