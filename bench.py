@@ -131,7 +131,8 @@ class Workload:
         wall = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-            t = torch.tensor([wall], dtype=torch.float64, device=dev)
+            on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor([wall], dtype=torch.float64, device=on)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             wall = float(t.item())
         region_ms = r0.elapsed_time(r1)
@@ -316,10 +317,18 @@ def main(argv=None) -> int:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device")
+    # MH_BENCH_BACKEND=gloo rehearses the multi-rank path on a one-GPU box (every
+    # rank on the same device, CPU collectives); the driver's runs use RCCL
+    backend = os.environ.get("MH_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import metalhuffman_amd as mh
     import metalhuffman_amd.build as B
@@ -335,6 +344,9 @@ def main(argv=None) -> int:
     if world > 1:
         # 256-byte canonical header over RCCL; each GPU builds T1/T2 + its decode table
         canon = mh.encode_frame(bb).canon if rank == 0 else None
+        # the first broadcast also creates the communicator and loads the table-build
+        # kernel; the second one is timed
+        MD.broadcast_header_device_tables(canon, src=0, device=dev).check_status()
         torch.cuda.synchronize(dev)
         dist.barrier()
         tb = time.perf_counter()
