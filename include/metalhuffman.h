@@ -118,6 +118,18 @@ typedef struct {
 int mh_decode(const mh_frame *frame, uint8_t *d_out, size_t out_pitch,
               size_t out_frame_stride, void *stream);
 
+/* Debug mode of the decode contract: walks every block of
+ * `frame` exactly as mh_decode does and writes, per frame f, u32 d_report[4f..4f+3]:
+ *   [0] zero-width lookups (windows no code matches -- the reference's {0,0}
+ *       entry, HuffmanUtil.cpp:550-556, which repeats prev without advancing),
+ *   [1] T1 escapes to a subtable at or past table2_entries (table index > k),
+ *   [2] blocks whose 64 codes do not end at the next block's offset
+ *       (a frame's last block is not checked),
+ *   [3] the first such block (frame relative), or 0xFFFFFFFF.
+ * Never writes the raster; valid reference streams report 0, 0, 0, 0xFFFFFFFF.
+ * Asynchronous on `stream`. */
+int mh_check(const mh_frame *frame, uint32_t *d_report, void *stream);
+
 /* Bytes needed for the derived lookup table mh_prepare_lut() writes. */
 size_t mh_lut_bytes(void);
 

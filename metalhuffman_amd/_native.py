@@ -26,7 +26,7 @@ EXPORTS = (
     "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
     "mh_stream_compute_stream", "mh_stream_wait", "mh_stream_synchronize", "mh_stream_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
-    "mh_container_header", "mh_parse_container_header",
+    "mh_container_header", "mh_parse_container_header", "mh_check",
 )
 
 
@@ -77,6 +77,7 @@ def lib() -> ctypes.CDLL:
                 "(the HIP decoder has no fallback)")
         L = ctypes.CDLL(LIB_PATH)
         L.mh_decode.argtypes = [ctypes.POINTER(mh_frame), _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]
+        L.mh_check.argtypes = [ctypes.POINTER(mh_frame), _vp, _vp]
         L.mh_lut_bytes.restype = ctypes.c_size_t
         L.mh_lut_bits.restype = ctypes.c_int
         L.mh_prepare_lut.argtypes = [_vp, _vp, ctypes.c_uint32, _vp, _vp]

@@ -28,6 +28,8 @@ SOURCES = {
                                       "-Wall", "-c"]),
     "mh_encode.o": ("mh_encode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
+    "mh_check.o": ("mh_check.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+                                    "-Wall", "-c"]),
     "mh_stream.o": ("mh_stream.cpp", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
     "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),

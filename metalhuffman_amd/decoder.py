@@ -184,6 +184,22 @@ def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tenso
     return out
 
 
+CHECK_FIELDS = ("zero_width_lookups", "bad_escapes", "length_mismatches", "first_bad_block")
+
+
+def check(frames: DeviceFrames, tables: DeviceTables,
+          stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """Debug mode of the decode contract (mh_check): per frame u32[4] =
+    (zero-width lookups, T1 escapes past T2, blocks whose codes miss the next
+    block's offset, first offending block or 0xFFFFFFFF), as an int64 tensor
+    [n_frames, 4] on the device. Never touches a raster."""
+    dev = frames.codes.device
+    rep = torch.empty((frames.n_frames, 4), dtype=torch.int32, device=dev)
+    fr = _frame_struct(frames, tables)
+    N.check(N.lib().mh_check(ctypes.byref(fr), rep.data_ptr(), _stream_ptr(stream, dev)), "mh_check")
+    return rep.to(torch.int64) & 0xFFFFFFFF
+
+
 def decode_frames(encoded: Sequence[EncodedFrame], device="cuda") -> np.ndarray:
     """Convenience: upload, decode, copy back; returns [n, H, W] uint8 on the host."""
     t1, t2 = encoded[0].tables()

@@ -313,6 +313,51 @@ int orc_decode_frame_shader(const uint32_t *block_offsets, const uint8_t *codes,
   return ORC_OK;
 }
 
+/* The decode contract's debug report (the product's mh_check):
+ * per block, the same 64 steps as AAPLShaders.metal:241-268, counting
+ * report[0] zero-width lookups ({0,0} entries, HuffmanUtil.cpp:550-556),
+ * report[1] T1 escapes to a subtable at/after t2_entries (counted as zero width),
+ * report[2] blocks (all but the last) whose codes end off the next block's offset,
+ * report[3] first offending block or 0xFFFFFFFF. Bytes past codes_bytes read 0. */
+void orc_check_frame(const uint32_t *block_offsets, const uint8_t *codes, uint64_t codes_bytes,
+                     const orc_sym *t1, const orc_sym *t2, uint32_t t2_entries, uint32_t nb,
+                     uint32_t report[4]) {
+  report[0] = report[1] = report[2] = 0;
+  report[3] = 0xFFFFFFFFu;
+  for (uint32_t b = 0; b < nb; b++) {
+    uint64_t pos = block_offsets[b];
+    uint32_t zw = 0, esc = 0;
+    for (int k = 0; k < 64; k++) {
+      const uint64_t i = pos >> 3;
+      const uint32_t m = (uint32_t)(pos & 7);
+      const uint32_t b0 = i < codes_bytes ? codes[i] : 0;
+      const uint32_t b1 = i + 1 < codes_bytes ? codes[i + 1] : 0;
+      const uint32_t b2 = i + 2 < codes_bytes ? codes[i + 2] : 0;
+      const uint32_t pat = ((((b0 << m) & 0xFF) << 8) | (b1 << m) | (b2 >> (8 - m))) & 0xFFFF;
+      orc_sym e = t1[pat >> 8];
+      if (e.bitWidth == 0) {
+        const uint32_t idx = (uint32_t)e.symbol * 256u + (pat & 0xFF);
+        if (idx < t2_entries) {
+          e = t2[idx];
+        } else {
+          esc++;
+          e.symbol = 0;
+          e.bitWidth = 0;
+        }
+      }
+      if (e.bitWidth == 0) zw++;
+      pos += e.bitWidth;
+    }
+    const int mism = b + 1 < nb && pos != block_offsets[b + 1];
+    if (zw || esc || mism) {
+      report[0] += zw;
+      report[1] += esc;
+      report[2] += (uint32_t)mism;
+      if (b < report[3]) report[3] = b;
+    }
+  }
+}
+
 /* AAPLRenderer.m:374-688 (setupHuffmanEncoding) for blockDim 8, deltas on. */
 int orc_encode_frame(const uint8_t *img, uint32_t w, uint32_t h, uint8_t canon[256],
                      uint8_t *codes, uint64_t codes_cap, uint64_t *codes_len,

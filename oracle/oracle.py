@@ -67,6 +67,8 @@ def lib():
                                              ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_time_decode_frames.restype = ctypes.c_double
+        L.orc_check_frame.argtypes = [_u32p, _u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_uint32,
+                                      ctypes.c_uint32, _u32p]
         _lib = L
     return _lib
 
@@ -178,6 +180,18 @@ def decode_frame_shader(offsets, codes, t1, t2, w, h, block_init=None, delta=Tru
                                          bw, bh, _p(bi) if bi is not None else None,
                                          1 if delta else 0, _p(out)), "decode_frame_shader")
     return out
+
+
+def check_frame(offsets, codes, t1, t2) -> np.ndarray:
+    """Debug report of one frame (see orc_check_frame): u32[4]."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    t1 = np.ascontiguousarray(t1, dtype=np.uint8)
+    t2 = np.ascontiguousarray(t2, dtype=np.uint8)
+    rep = np.zeros(4, np.uint32)
+    lib().orc_check_frame(_p(offsets, _u32p), _p(codes), ctypes.c_uint64(codes.size), _p(t1), _p(t2),
+                          ctypes.c_uint32(t2.size // 2), ctypes.c_uint32(offsets.size), _p(rep, _u32p))
+    return rep
 
 
 def encode_frame(img: np.ndarray):

@@ -110,6 +110,12 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_encode_frame_device(0x100, 8, 8, 0, canon, 0x1000, 64, ctypes.byref(n), 0x2000, None,
                                     0x10000, 16, None) == -4
     assert L.mh_encode_workspace_bytes(2048, 1536) >= 49152 * 64
+    assert L.mh_check(None, 0x70000, None) == -1
+    assert L.mh_check(ctypes.byref(_frame()), None, None) == -1
+    assert L.mh_check(ctypes.byref(_frame(n_frames=2)), 0x70000, None) == -1
+    assert L.mh_check(ctypes.byref(_frame(dims=N.mh_dims(2048, 1536, 255, 192))), 0x70000, None) == -2
+    assert L.mh_check(ctypes.byref(_frame(table2_entries=100)), 0x70000, None) == -5
+    assert L.mh_check(ctypes.byref(_frame()), 0x70002, None) == -6
 
 
 def test_constants(mh):
