@@ -32,6 +32,7 @@ import json
 import os
 import sys
 import time
+import zlib
 
 import numpy as np
 import torch
@@ -412,6 +413,14 @@ def main(argv=None) -> int:
         args.workload, lambda: F.block_shuffle(bb, seeds[0]))()
     if not np.array_equal(chk, ref_img) and not os.environ.get("MH_LIB"):
         raise SystemExit("bench: decoded frame differs from the encoder input")
+    # every rank's CRC32 of its first decoded frame, gathered on rank 0 and compared
+    # with the CRC32 of that rank's input frame (SURVEY.md 8(e) verification)
+    crcs_ok = None
+    if world > 1:
+        mine = (zlib.crc32(chk.tobytes()), zlib.crc32(ref_img.tobytes()))
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        crcs_ok = sum(1 for a, b in got if a == b)
 
     wall, region_ms, kms = wl.run(args.steps, args.warmup, use_graph=not args.no_graph, world=world)
     per_step = wall / args.steps
@@ -430,6 +439,8 @@ def main(argv=None) -> int:
         "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload),
         "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
     }
+    if crcs_ok is not None:
+        result["ranks_crc32_verified"] = crcs_ok
     if t_bcast_us is not None:
         result["table_broadcast_us"] = round(t_bcast_us, 1)  # 256-B RCCL broadcast + device table build
         result["table_broadcast_bytes"] = 256

@@ -55,6 +55,9 @@ namespace {
 #ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
 #define MH_SMALL_KERNEL 1
 #endif
+#ifndef MH_MASKED_REFILL        // 1: in the batch kernel, only lanes that consumed a word
+#define MH_MASKED_REFILL 1      //    read the next one (fewer LDS bank conflicts)
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -245,16 +248,17 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 // kSpec: the table address of a pair's first symbol is taken from whichever
 //   window the refill selects (two shifts in parallel), taking the word move off
 //   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
-template <int kBits, bool kSpecRefill>
+template <int kBits, bool kSpecRefill, bool kMaskedRefill = false>
 struct StepCfg {
   static constexpr bool kEsc = kBits == kLutBits;
   static constexpr bool kSpec = kSpecRefill;
+  static constexpr bool kMasked = kMaskedRefill && !kSpecRefill;
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
   static constexpr uint32_t kMask = (2u << kBits) - 2u;       // byte address of a u16 entry
   static constexpr uint32_t kRefillAt = kCur - 32u;           // low byte <= this: sh >= 32
 };
 
-using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0>;  // the batch kernel's step
+using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  // the batch kernel's step
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -315,7 +319,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     const uint32_t d = c ? 4u : 0u;                                                 \
     wa += d;                                                                        \
     S += d * 8u;                                                                    \
-    nw = word_at(wa + 8);                                                           \
+    if constexpr (!Cfg::kMasked) nw = word_at(wa + 8);                              \
   }
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
@@ -329,6 +333,11 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     } else {                                                                        \
       MH_REFILL_C(c)                                                                \
       MH_STEP(J, OW)                                                                \
+      /* masked: only lanes that consumed a word fetch the next (issued behind */   \
+      /* the lookup; fewer active lanes -> fewer LDS bank conflicts)          */   \
+      if constexpr (Cfg::kMasked) {                                                 \
+        if (c) nw = word_at(wa + 8);                                                \
+      }                                                                             \
     }                                                                               \
   }
 
