@@ -55,6 +55,9 @@ namespace {
 #ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
 #define MH_SMALL_KERNEL 1
 #endif
+#ifndef MH_NOESC_PATH           // 1: batch kernel steps without the escape test when the
+#define MH_NOESC_PATH 1         //    prepared table's longest code is <= 13 bits
+#endif
 #ifndef MH_MASKED_REFILL        // 1: in the batch kernel, only lanes that consumed a word
 #define MH_MASKED_REFILL 1      //    read the next one (fewer LDS bank conflicts)
 #endif
@@ -248,9 +251,9 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 // kSpec: the table address of a pair's first symbol is taken from whichever
 //   window the refill selects (two shifts in parallel), taking the word move off
 //   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
-template <int kBits, bool kSpecRefill, bool kMaskedRefill = false>
+template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits>
 struct StepCfg {
-  static constexpr bool kEsc = kBits == kLutBits;
+  static constexpr bool kEsc = kEscapes;
   static constexpr bool kSpec = kSpecRefill;
   static constexpr bool kMasked = kMaskedRefill && !kSpecRefill;
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
@@ -259,6 +262,9 @@ struct StepCfg {
 };
 
 using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  // the batch kernel's step
+// ... and its escape-free twin, for tables whose longest code is <= 13 bits (the
+// first level then decodes every window; no per-symbol escape test)
+using Lut13NoEsc = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -616,6 +622,10 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   MH_STAMP(0);
 
   uint32_t prio = blockIdx.x * nwaves + wave;  // rotation phase (MH_PRIO_ROTATE 1, 2)
+  // prepared table with no code longer than 13 bits: escape-free steps
+  const bool no_esc = MH_NOESC_PATH && a.lut &&
+                      *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) +
+                                                          kMaxLenOff) <= (uint32_t)kLutBits;
   // static grid-stride schedule; a tile id >= total_tiles means "no tile"
   const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
@@ -670,8 +680,12 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
       // waves with more tiles left run first (the arbiter otherwise favours the oldest)
       set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
 #endif
-      decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
-                                  prio);
+      if (no_esc)
+        decode_block<kDelta, Lut13NoEsc>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch,
+                                         dead, prio);
+      else
+        decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
+                                    prio);
       prio += MH_PRIO_ROTATE == 2 ? 3u : 1u;
     }
 #if MH_DIAG_STAMPS

@@ -257,3 +257,19 @@ def test_small_batch_kernel_boundary(mh, device, bigbridge, h):
     ef = mh.encode_frame(img)
     out = _decode([ef], device)[0]
     assert np.array_equal(out, img)
+
+
+@pytest.mark.parametrize("n_sym", [14, 15])
+def test_batch_kernel_code_length_paths(mh, oracle, device, n_sym):
+    """20 frames x 64 tiles (> the small kernel's limit): longest code 13 bits takes
+    the batch kernel's escape-free step, 14 bits the escape step."""
+    from metalhuffman_amd import frames as F
+    d = fibonacci_deltas(n_sym, 512 * 512, seed=30 + n_sym)
+    base = image_from_block_deltas(d, 512, 512)
+    imgs = [F.block_shuffle(base, 200 + s) for s in range(20)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    assert efs[0].canon.max() == n_sym - 1
+    out = _decode(efs, device)
+    for i, im in enumerate(imgs):
+        assert np.array_equal(out[i], im), i
+    assert np.array_equal(out[7], _oracle_decode(oracle, efs[7]))
