@@ -87,11 +87,32 @@ def build_variant(name: str, defines: list[str], verbose: bool = False,
     return out
 
 
+HOST_SRC = os.path.join(ROOT, "host", "mh_decode_host.c")
+HOST_BIN = os.path.join(ROOT, "host", "mh_decode_host")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """The plain-C host program (host/mh_decode_host.c): gcc against the C-ABI
+    header, libmetalhuffman_amd.so and the HIP runtime's C API."""
+    lib = build(force=force, verbose=verbose)
+    if force or _stale(HOST_BIN, [HOST_SRC, lib] + HEADERS):
+        cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-D__HIP_PLATFORM_AMD__",
+               "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROCM, "include"), HOST_SRC,
+               "-o", HOST_BIN, "-L", PKG, "-lmetalhuffman_amd", "-L", os.path.join(ROCM, "lib"),
+               "-lamdhip64", f"-Wl,-rpath,$ORIGIN/../metalhuffman_amd:{os.path.join(ROCM, 'lib')}"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return HOST_BIN
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     args = ap.parse_args(argv)
     print(build(force=args.force, verbose=True))
+    print(build_host(force=args.force, verbose=True))
     return 0
 
 

@@ -273,3 +273,34 @@ def test_batch_kernel_code_length_paths(mh, oracle, device, n_sym):
     for i, im in enumerate(imgs):
         assert np.array_equal(out[i], im), i
     assert np.array_equal(out[7], _oracle_decode(oracle, efs[7]))
+
+
+def test_fuzz_shapes_and_histograms(mh, oracle, device):
+    """Seeded fuzz: 40 frames of random size (1..700 each side), random symbol
+    histograms (geometric / two-sided / uniform), all three formats, prepared and
+    in-kernel tables; every output equals the oracle's shader-semantics decode."""
+    r = np.random.default_rng(2024)
+    done = 0
+    for i in range(60):
+        h, w = int(r.integers(1, 701)), int(r.integers(1, 701))
+        kind = i % 3
+        if kind == 0:
+            img = np.minimum(r.geometric(r.uniform(0.05, 0.6), size=(h, w)) - 1, 255).astype(np.uint8)
+            img = np.cumsum(img, axis=1, dtype=np.uint8)
+        elif kind == 1:
+            img = (np.round(r.normal(128, r.uniform(1, 30), size=(h, w))) % 256).astype(np.uint8)
+        else:
+            img = r.integers(0, 256, size=(h, w), dtype=np.uint8)
+        fmt = int(r.integers(0, 3))
+        kw = {"flags": mh.MH_FLAG_NO_DELTA} if fmt == 1 else ({"init_zero_delta": True} if fmt == 2 else {})
+        try:
+            ef = mh.encode_frame(img, **kw)
+        except mh.MHError:
+            continue  # a code deeper than 16 bits: invalid for the reference too
+        out = _decode([ef], device, prepared=bool(i % 2))[0]
+        assert np.array_equal(out, img), (i, h, w, kind, fmt)
+        assert np.array_equal(out, _oracle_decode(oracle, ef)), (i, h, w, kind, fmt)
+        done += 1
+        if done == 40:
+            break
+    assert done >= 30

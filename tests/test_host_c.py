@@ -1,0 +1,70 @@
+"""The plain-C host program (host/mh_decode_host.c) over the C-ABI: builds with gcc
+against include/metalhuffman.h and, on the GPU, decodes bit-exactly -- including
+buffers exactly as the reference encoder emitted them (golden.json)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import golden
+
+
+@pytest.fixture(scope="module")
+def host_bin(mh):
+    import metalhuffman_amd.build as B
+    return B.build_host()
+
+
+def _run(args, timeout=120):
+    return subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+
+
+def test_host_builds_and_prints_usage(host_bin):
+    r = _run([host_bin])
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wh", [(2048, 1536), (1001, 777), (8, 8), (13, 5)])
+def test_host_synth(host_bin, wh):
+    r = _run([host_bin, "synth", str(wh[0]), str(wh[1]), "5"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith(f"decode ok {wh[0]} {wh[1]} "), r.stdout
+    assert " check 0 0 0 " in r.stdout  # mh_check: a clean stream
+
+
+@pytest.mark.gpu
+def test_host_raw_bigbridge(host_bin, bigbridge, tmp_path):
+    p = tmp_path / "bb.gray"
+    p.write_bytes(np.ascontiguousarray(bigbridge).tobytes())
+    h, w = bigbridge.shape
+    r = _run([host_bin, "raw", str(w), str(h), str(p), "20"])
+    assert r.returncode == 0 and r.stdout.startswith(f"decode ok {w} {h} "), r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_host_reference_encoder_buffers(host_bin, tmp_path):
+    """The reference encoder's own canonical header, codes and block offsets
+    (golden.json) decoded unchanged by the C host."""
+    n = 0
+    for name, fx in golden()["small_frames"].items():
+        w, h = fx["width"], fx["height"]
+        canon = np.zeros(256, np.uint8)
+        for k, v in fx["canon"].items():
+            canon[int(k)] = v
+        files = {"canon": canon.tobytes(), "codes": bytes.fromhex(fx["codes_hex"]),
+                 "offsets": np.array(fx["block_offsets"], "<u4").tobytes(),
+                 "expected": np.array(fx["pixels"], np.uint8).tobytes()}
+        paths = []
+        for k, v in files.items():
+            p = tmp_path / f"{name}.{k}"
+            p.write_bytes(v)
+            paths.append(str(p))
+        r = _run([host_bin, "buffers", str(w), str(h)] + paths)
+        assert r.returncode == 0, (name, r.stdout, r.stderr)
+        assert r.stdout.startswith(f"decode ok {w} {h} "), (name, r.stdout)
+        n += 1
+    assert n >= 5
