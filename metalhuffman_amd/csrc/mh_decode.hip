@@ -55,6 +55,9 @@ namespace {
 #ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
 #define MH_SMALL_KERNEL 1
 #endif
+#ifndef MH_STAGE_SWIZZLE        // 1: flat tables (one code length) stage chunks XOR-permuted
+#define MH_STAGE_SWIZZLE 1      //    within 128-B rows (batch kernel)
+#endif
 #ifndef MH_NOESC_PATH           // 1: batch kernel steps without the escape test when the
 #define MH_NOESC_PATH 1         //    prepared table's longest code is <= 13 bits
 #endif
@@ -78,7 +81,7 @@ constexpr int kLut14Bits = 14;
 constexpr int kLut14Entries = 1 << kLut14Bits;           // 16384 x u16
 constexpr int kLut14Off = kLutBytes;                     // byte offset in the buffer
 constexpr int kLut14Bytes = kLut14Entries * 2;           // 32768
-constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest code length
+constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest, u32 shortest code length
 constexpr int kPreparedBytes = kMaxLenOff + 16;          // 51248
 constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile span)
 constexpr int kMaxWavesPerWG = MH_MAX_WAVES;
@@ -176,27 +179,35 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
 // Single-level 14-bit table: step_word of every window whose code has <= 14 bits
 // (0 otherwise), and the longest code length of the table into *max_len.
 __device__ void build_lut14(const uint16_t *t1, const uint16_t *t2, uint32_t t2_entries,
-                            uint16_t *lut14, uint32_t *max_len, uint32_t tid, uint32_t nthreads) {
-  uint32_t mx = 0;
+                            uint16_t *lut14, uint32_t *max_len, uint32_t *min_len, uint32_t tid,
+                            uint32_t nthreads) {
+  uint32_t mx = 0, mn = 255;
   for (uint32_t p = tid; p < (uint32_t)kLut14Entries; p += nthreads) {
     const uint32_t e = split_lookup(t1, t2, t2_entries, p << (16 - kLut14Bits));
     const uint32_t len = e >> 8;
     lut14[p] = (uint16_t)(len <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
     mx = max(mx, len);
+    if (len) mn = min(mn, len);
   }
   atomicMax(max_len, mx);
+  atomicMin(min_len, mn);
 }
 
 __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1, const uint16_t *t2,
                                                               uint32_t t2_entries, uint8_t *buf) {
-  __shared__ uint32_t p0, mx;
-  if (threadIdx.x == 0) mx = 0;
+  __shared__ uint32_t p0, mx, mn;
+  if (threadIdx.x == 0) {
+    mx = 0;
+    mn = 255;
+  }
   build_lut(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf), &p0, threadIdx.x, blockDim.x,
             [] { __syncthreads(); });
-  build_lut14(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf + kLut14Off), &mx, threadIdx.x,
+  build_lut14(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf + kLut14Off), &mx, &mn, threadIdx.x,
               blockDim.x);
   __syncthreads();
-  if (threadIdx.x < 4) reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[threadIdx.x] = threadIdx.x ? 0u : mx;
+  // [longest code, shortest code, 0, 0]
+  if (threadIdx.x < 4)
+    reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[threadIdx.x] = threadIdx.x == 0 ? mx : threadIdx.x == 1 ? mn : 0u;
 }
 
 // Word source for the bit cursor: big-endian dwords of the tile's code span.
@@ -207,6 +218,12 @@ struct LdsWords {
 __device__ __forceinline__ uint32_t word_at(const uint8_t *q) {
   return *reinterpret_cast<const uint32_t *>(q);
 }
+// Stage swizzle (batch kernel, MH_STAGE_SWIZZLE): the eight 16-B chunks of every
+// 128-B row of a wave's stage are permuted by the row index (XOR), so lanes whose
+// blocks start a multiple of 128 B apart -- flat code lengths make every block
+// exactly 64 B -- refill from different LDS banks (b32 reads bank on (a/4) mod 32).
+// Chunks stay whole (16-B staging stores) and stay inside their row.
+__device__ __forceinline__ uint32_t swz_off(uint32_t o) { return o ^ ((o >> 3) & 0x70u); }
 
 // byte 1 (prev) of four successive lane states -> one output word, 3 VALU
 __device__ __forceinline__ uint32_t pack_prev4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -251,9 +268,11 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 // kSpec: the table address of a pair's first symbol is taken from whichever
 //   window the refill selects (two shifts in parallel), taking the word move off
 //   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
-template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits>
+template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits,
+          bool kSwizzle = false>
 struct StepCfg {
   static constexpr bool kEsc = kEscapes;
+  static constexpr bool kSwz = kSwizzle;
   static constexpr bool kSpec = kSpecRefill;
   static constexpr bool kMasked = kMaskedRefill && !kSpecRefill;
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
@@ -265,6 +284,10 @@ using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  //
 // ... and its escape-free twin, for tables whose longest code is <= 13 bits (the
 // first level then decodes every window; no per-symbol escape test)
 using Lut13NoEsc = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false>;
+// ... and for flat tables (every code the same length, e.g. uniform bytes: every
+// block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
+using Lut13Flat = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false,
+                          MH_STAGE_SWIZZLE != 0>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -283,10 +306,16 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
                                              uint32_t row0, uint32_t pitch, bool dead,
                                              uint32_t prio = 0) {
   const uint8_t *wa = src.at((p >> 5) * 4u);
+  const auto rd = [&](const uint8_t *q) -> uint32_t {
+    if constexpr (Cfg::kSwz)
+      return word_at(src.w + swz_off((uint32_t)(q - src.w)));
+    else
+      return word_at(q);
+  };
   uint32_t S = (prev << 8) + Cfg::kCur - (p & 31u);
-  uint32_t hi = word_at(wa);
-  uint32_t lo = word_at(wa + 4);
-  uint32_t nw = word_at(wa + 8);
+  uint32_t hi = rd(wa);
+  uint32_t lo = rd(wa + 4);
+  uint32_t nw = rd(wa + 8);
   (void)prio;
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
@@ -325,7 +354,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     const uint32_t d = c ? 4u : 0u;                                                 \
     wa += d;                                                                        \
     S += d * 8u;                                                                    \
-    if constexpr (!Cfg::kMasked) nw = word_at(wa + 8);                              \
+    if constexpr (!Cfg::kMasked) nw = rd(wa + 8);                                   \
   }
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
@@ -342,7 +371,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
       /* masked: only lanes that consumed a word fetch the next (issued behind */   \
       /* the lookup; fewer active lanes -> fewer LDS bank conflicts)          */   \
       if constexpr (Cfg::kMasked) {                                                 \
-        if (c) nw = word_at(wa + 8);                                                \
+        if (c) nw = rd(wa + 8);                                                     \
       }                                                                             \
     }                                                                               \
   }
@@ -535,6 +564,7 @@ __device__ __forceinline__ void span_issue(const DecodeArgs &a, const Tile &t, u
   }
 }
 
+template <bool kSwz = false>
 __device__ __forceinline__ void span_write(const Tile &t, uint32_t lane, const v4u32 (&R)[kStageChunks],
                                            uint8_t *stage) {
 #pragma unroll
@@ -546,7 +576,7 @@ __device__ __forceinline__ void span_write(const Tile &t, uint32_t lane, const v
       v.y = bswap32(v.y);
       v.z = bswap32(v.z);
       v.w = bswap32(v.w);
-      *reinterpret_cast<v4u32 *>(stage + c * 16u) = v;
+      *reinterpret_cast<v4u32 *>(stage + (kSwz ? swz_off(c * 16u) : c * 16u)) = v;
     }
   }
 }
@@ -589,7 +619,7 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
       v.y = bswap32(v.y);
       v.z = bswap32(v.z);
       v.w = bswap32(v.w);
-      *reinterpret_cast<v4u32 *>(stage + c * 16u) = v;
+      *reinterpret_cast<v4u32 *>(stage + (Cfg::kSwz ? swz_off(c * 16u) : c * 16u)) = v;
     }
     wave_sync();
     if (lane >= first && lane < first + 32u) {
@@ -607,8 +637,9 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
 // Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
 // header of tile i+2 and the code span of tile i+1 are in flight into registers;
 // the span is written to the wave's LDS window once tile i has finished reading it.
-template <bool kDelta>
-__global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_decode_kernel(const DecodeArgs a) {
+template <bool kDelta, class Cfg>
+__device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
+  constexpr bool kSwz = Cfg::kSwz;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = blockDim.x >> 6;
@@ -622,10 +653,6 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   MH_STAMP(0);
 
   uint32_t prio = blockIdx.x * nwaves + wave;  // rotation phase (MH_PRIO_ROTATE 1, 2)
-  // prepared table with no code longer than 13 bits: escape-free steps
-  const bool no_esc = MH_NOESC_PATH && a.lut &&
-                      *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) +
-                                                          kMaxLenOff) <= (uint32_t)kLutBits;
   // static grid-stride schedule; a tile id >= total_tiles means "no tile"
   const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
@@ -652,7 +679,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
   MH_STAMP(2);
-  if (cur_staged) span_write(cur, lane, R, stage);
+  if (cur_staged) span_write<kSwz>(cur, lane, R, stage);
   MH_STAMP(3);
   // Resolved even past the end (zero-record loads): every Tile field is defined
   // before span_issue builds a descriptor from it.
@@ -680,12 +707,8 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
       // waves with more tiles left run first (the arbiter otherwise favours the oldest)
       set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
 #endif
-      if (no_esc)
-        decode_block<kDelta, Lut13NoEsc>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch,
-                                         dead, prio);
-      else
-        decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
-                                    prio);
+      decode_block<kDelta, Cfg>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
+                                prio);
       prio += MH_PRIO_ROTATE == 2 ? 3u : 1u;
     }
 #if MH_DIAG_STAMPS
@@ -693,7 +716,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     first_tile = false;
 #endif
     wave_sync();  // this tile's reads -> next tile's staging writes
-    if (nxt_staged) span_write(nxt, lane, R, stage);
+    if (nxt_staged) span_write<kSwz>(nxt, lane, R, stage);
     const Tile nn = hdr_resolve(a, hn, lane);
     cur = nxt;
     cur_staged = nxt_staged;
@@ -709,7 +732,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     hdr_issue(a, t, lane, h);
     const Tile tt = hdr_resolve(a, h, lane);
     const OutTile ot = out_tile(a, tt, lane);
-    decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+    decode_halves<kDelta, Cfg>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
   }
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
@@ -721,6 +744,26 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
   if (lane == 0 && gw < (uint32_t)kDiagWaves)
     for (int i = 0; i < kDiagSlots; ++i) g_stamps[gw * kDiagSlots + i] = ts[i];
 #endif
+}
+
+// The batch kernel: one instantiation of the persistent loop per step flavour,
+// chosen from the prepared table's code lengths (kernel-uniform): no code longer
+// than 13 bits -> escape-free; one code length only -> escape-free with the
+// swizzled stage. An in-kernel table (no prepared LUT) keeps the general step.
+template <bool kDelta>
+__global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_decode_kernel(const DecodeArgs a) {
+  uint32_t mx = 16, mn = 0;
+  if (a.lut) {
+    const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
+    mx = ml[0];
+    mn = ml[1];
+  }
+  if (MH_STAGE_SWIZZLE && a.lut && mx == mn)
+    batch_tiles<kDelta, Lut13Flat>(a);
+  else if (MH_NOESC_PATH && a.lut && mx <= (uint32_t)kLutBits)
+    batch_tiles<kDelta, Lut13NoEsc>(a);
+  else
+    batch_tiles<kDelta, Lut13>(a);
 }
 
 // ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------

@@ -304,3 +304,17 @@ def test_fuzz_shapes_and_histograms(mh, oracle, device):
         if done == 40:
             break
     assert done >= 30
+
+
+def test_batch_kernel_flat_table(mh, oracle, device):
+    """Uniform random bytes: every code 8 bits (a flat table), every block exactly
+    64 bytes -> the batch kernel's swizzled-stage step; 5 x 1024^2 = 1280 tiles."""
+    from metalhuffman_amd import frames as F
+    base = F.uniform_random(1024, 1024, 77)
+    imgs = [base] + [F.block_shuffle(base, 300 + s) for s in range(4)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    assert efs[0].canon.min() == efs[0].canon.max() == 8
+    out = _decode(efs, device)
+    for i, im in enumerate(imgs):
+        assert np.array_equal(out[i], im), i
+    assert np.array_equal(out[3], _oracle_decode(oracle, efs[3]))
