@@ -64,6 +64,12 @@ namespace {
 #ifndef MH_MASKED_REFILL        // 1: in the batch kernel, only lanes that consumed a word
 #define MH_MASKED_REFILL 1      //    read the next one (fewer LDS bank conflicts)
 #endif
+#ifndef MH_SMALL_SPEC           // small-launch kernel step: 1 refill off the chain (kSpec; 1.2 % slower)
+#define MH_SMALL_SPEC 0
+#endif
+#ifndef MH_SMALL_MASKED         // small-launch kernel: masked refill reads (kSpec 0 only)
+#define MH_SMALL_MASKED 0
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -370,7 +376,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
       MH_STEP(J, OW)                                                                \
       /* masked: only lanes that consumed a word fetch the next (issued behind */   \
       /* the lookup; fewer active lanes -> fewer LDS bank conflicts)          */   \
-      if constexpr (Cfg::kMasked) {                                                 \
+      if constexpr (Cfg::kMasked) {                              \
         if (c) nw = rd(wa + 8);                                                     \
       }                                                                             \
     }                                                                               \
@@ -831,10 +837,10 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
     MH_STAMP(3);
     LdsWords src{stage};
     if (l14)
-      decode_block<kDelta, StepCfg<kLut14Bits, true>>(src, lut, t.p, t.init, out, row0,
+      decode_block<kDelta, StepCfg<kLut14Bits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0>>(src, lut, t.p, t.init, out, row0,
                                                       (uint32_t)a.out_pitch, !t.valid);
     else
-      decode_block<kDelta, StepCfg<kLutBits, true>>(src, lut, t.p, t.init, out, row0,
+      decode_block<kDelta, StepCfg<kLutBits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0>>(src, lut, t.p, t.init, out, row0,
                                                     (uint32_t)a.out_pitch, !t.valid);
   } else if (l14) {
     decode_halves<kDelta, StepCfg<kLut14Bits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
