@@ -163,11 +163,16 @@ def measured_traffic(workload: str):
         return None
 
 
+ACHIEVABLE = {}  # filled from hbm_probe() before the roofline lines (rank 0, N=1)
+
+
 def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
     """achieved = algorithmic bytes of one launch / the launch's average duration,
     the latter from the HIP events bracketing the timed hipGraph replay on its
     stream (the K kernels run back to back there, so region / K is the kernel
-    duration rocprofv3's kernel trace reports for the same command)."""
+    duration rocprofv3's kernel trace reports for the same command).
+    frac is against the 8 TB/s spec; frac_of_achievable against a plain streaming
+    kernel with the decoder's read:write mix measured on the same box."""
     avg_s = region_ms * 1e-3 / steps
     ach = bytes_per_launch / avg_s / 1e9
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -175,6 +180,10 @@ def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
          "traffic": measured_traffic(workload) if workload else None,
          "kernel_us_avg": round(avg_s * 1e6, 3),
          "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    mix = ACHIEVABLE.get("mix_2r3w_GBps")
+    if mix:
+        r["achievable_mix_GBps"] = mix
+        r["frac_of_achievable"] = round(ach / mix, 4)
     if eager_ms:
         # one launch at a time with an event pair each (includes launch latency)
         r["eager_launch_us_median"] = round(float(np.median(eager_ms)) * 1e3, 3)
@@ -247,6 +256,27 @@ def copy_bandwidth(device, nbytes=1 << 30, reps=20):
     del a, b
     return {"bytes_moved": 2 * nbytes, "best_ms": round(best, 4),
             "GBps": round(2 * nbytes / (best * 1e-3) / 1e9, 1), "kernel": "torch copy_ (D2D)"}
+
+
+def hbm_probe(nbytes=1 << 30, reps=10):
+    """Achievable HBM bandwidth on this box from scripts/micro/libhbm_probe.so (16-B
+    vector streams, every CU busy): copy, read-only, write-only and the decoder's
+    read:write mix (2:3), with non-temporal stores (as the decoder) and with
+    default-policy stores. None when the probe was not built."""
+    import ctypes
+    path = os.path.join(ROOT, "scripts", "micro", "libhbm_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.hbm_probe.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    out = {}
+    for mode, name in ((0, "copy"), (1, "read"), (2, "write"), (3, "mix_2r3w"), (4, "copy_plainstore"),
+                       (5, "write_plainstore"), (6, "mix_2r3w_plainstore")):
+        g = ctypes.c_double()
+        rc = lib.hbm_probe(mode, nbytes, reps, ctypes.byref(g))
+        out[name + "_GBps"] = round(g.value, 1) if rc == 0 else None
+    out["bytes_per_run"] = nbytes
+    return out
 
 
 def encode_rate(device, bb, reps=32):
@@ -424,6 +454,8 @@ def main(argv=None) -> int:
 
     wall, region_ms, kms = wl.run(args.steps, args.warmup, use_graph=not args.no_graph, world=world)
     per_step = wall / args.steps
+    if world == 1 and not args.no_extras:
+        ACHIEVABLE.update(hbm_probe() or {})  # after the timed region: the roofline context
     value = world * wl.pixels / per_step / 1e6
 
     result = {
@@ -464,6 +496,8 @@ def main(argv=None) -> int:
                             "roofline": roofline(w2.bytes, reg2, steps, kms2, key)}
             del w2
         extras["hbm_copy"] = copy_bandwidth(dev)  # achievable HBM rate beside the 8 TB/s spec
+        if ACHIEVABLE:
+            extras["hbm_probe"] = dict(ACHIEVABLE)
         extras["stream_h2d"] = stream_h2d(efs, tables, dev)  # config 5, one GPU
         extras["encode"] = encode_rate(dev, bb)
         result["extras"] = extras

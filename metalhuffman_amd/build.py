@@ -107,12 +107,29 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return HOST_BIN
 
 
+PROBE_SRC = os.path.join(ROOT, "scripts", "micro", "hbm_probe.hip")
+PROBE_LIB = os.path.join(ROOT, "scripts", "micro", "libhbm_probe.so")
+
+
+def build_probe(force: bool = False, verbose: bool = False) -> str:
+    """The achievable-HBM probe bench.py reports beside the roofline (measurement
+    infrastructure, not the decoder): scripts/micro/libhbm_probe.so."""
+    if force or _stale(PROBE_LIB, [PROBE_SRC]):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-Wno-unused-result",
+               "-o", PROBE_LIB, PROBE_SRC]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return PROBE_LIB
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     args = ap.parse_args(argv)
     print(build(force=args.force, verbose=True))
     print(build_host(force=args.force, verbose=True))
+    print(build_probe(force=args.force, verbose=True))
     return 0
 
 

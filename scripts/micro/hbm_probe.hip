@@ -1,0 +1,103 @@
+// hbm_probe.hip -- achievable HBM bandwidth on the box (measurement infrastructure for
+// bench.py's roofline context; not part of the decoder). Streams 16-B vectors with
+// non-temporal stores, grid-stride, every CU busy:
+//   mode 0 copy (read N, write N), 1 read-only, 2 write-only,
+//   mode 3 the decoder's mix: read 2 vectors, write 3 (2.12 MB read : 3.15 MB written per
+//          2048x1536 frame is 0.67; 2:3 is the nearest whole-vector ratio);
+//   modes 4-6: copy, write-only and the mix with default-policy (not nt) stores.
+// Built by metalhuffman_amd.build.build_probe() into scripts/micro/libhbm_probe.so.
+#include <hip/hip_runtime.h>
+
+#include <stddef.h>
+#include <stdint.h>
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <bool kNt, class T>
+__device__ __forceinline__ void st(const T &v, T *p) {
+  if (kNt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <int kMode, bool kNt = true>
+__global__ void __launch_bounds__(256) stream_kernel(const v4u *__restrict__ src, v4u *__restrict__ dst,
+                                                     size_t n_units, unsigned *sink) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  v4u acc = {0, 0, 0, 0};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_units; i += stride) {
+    if (kMode == 0) {
+      st<kNt>(src[i], &dst[i]);
+    } else if (kMode == 1) {
+      acc ^= src[i];
+    } else if (kMode == 2) {
+      v4u v = {(unsigned)i, 1u, 2u, 3u};
+      st<kNt>(v, &dst[i]);
+    } else {  // unit = 2 vectors read, 3 written, each stream coalesced
+      const v4u a = src[i], b = src[n_units + i];
+      st<kNt>(a, &dst[i]);
+      st<kNt>(b, &dst[n_units + i]);
+      st<kNt>(a ^ b, &dst[2 * n_units + i]);
+    }
+  }
+  if (kMode == 1 && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = 1;
+}
+
+extern "C" {
+
+// Best-of-reps bandwidth in GB/s (bytes read + written) over `bytes` of traffic.
+// Returns 0 on success.
+int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
+  if (mode < 0 || mode > 6 || !gbps || reps < 1) return -1;
+  const bool nt = mode < 4;
+  if (!nt) mode = mode == 4 ? 0 : mode == 5 ? 2 : 3;
+  const size_t unit_bytes = mode == 3 ? 5 * 16 : mode == 0 ? 32 : 16;
+  const size_t n_units = bytes / unit_bytes;
+  const size_t src_bytes = mode == 3 ? n_units * 32 : n_units * 16;
+  const size_t dst_bytes = mode == 3 ? n_units * 48 : n_units * 16;
+  void *src = nullptr, *dst = nullptr;
+  unsigned *sink = nullptr;
+  if (hipMalloc(&src, src_bytes) != hipSuccess || hipMalloc(&dst, dst_bytes) != hipSuccess ||
+      hipMalloc(&sink, 4) != hipSuccess)
+    return -2;
+  hipMemset(src, 1, src_bytes);
+  int dev = 0, cus = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const dim3 grid(cus * 16), block(256);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int r = 0; r < reps + 1; ++r) {
+    hipEventRecord(e0, 0);
+    const v4u *s = (const v4u *)src;
+    v4u *d = (v4u *)dst;
+    switch (mode + (nt ? 0 : 10)) {
+      case 0: hipLaunchKernelGGL(stream_kernel<0>, grid, block, 0, 0, s, d, n_units, sink); break;
+      case 1: hipLaunchKernelGGL(stream_kernel<1>, grid, block, 0, 0, s, d, n_units, sink); break;
+      case 2: hipLaunchKernelGGL(stream_kernel<2>, grid, block, 0, 0, s, d, n_units, sink); break;
+      case 3: hipLaunchKernelGGL(stream_kernel<3>, grid, block, 0, 0, s, d, n_units, sink); break;
+      case 10: hipLaunchKernelGGL((stream_kernel<0, false>), grid, block, 0, 0, s, d, n_units, sink); break;
+      case 12: hipLaunchKernelGGL((stream_kernel<2, false>), grid, block, 0, 0, s, d, n_units, sink); break;
+      default: hipLaunchKernelGGL((stream_kernel<3, false>), grid, block, 0, 0, s, d, n_units, sink); break;
+    }
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (r > 0 && ms < best) best = ms;  // first launch warms up
+  }
+  const double moved = mode == 1 ? (double)src_bytes : mode == 2 ? (double)dst_bytes
+                                                                  : (double)(src_bytes + dst_bytes);
+  *gbps = moved / (best * 1e-3) / 1e9;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(src);
+  hipFree(dst);
+  hipFree(sink);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // extern "C"
