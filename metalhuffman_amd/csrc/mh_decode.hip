@@ -773,11 +773,16 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 }
 
 // ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------
-// Every wave decodes one tile, so the per-symbol dependency chain (not LDS or VALU
-// throughput) sets the time: the step takes the refill off the chain (kSpec), and
-// when the table has no code longer than 14 bits the single-level 14-bit table
-// drops the escape test from it too.
-constexpr int kSmallWaves = 8;           // waves per workgroup (one tile each)
+// Every wave decodes one tile, one wave per SIMD: the wave's own instruction stream
+// (the per-symbol dependency chain and the instructions beside it), not LDS or VALU
+// throughput, sets the time. When the table has no code longer than 14 bits the
+// single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
+// SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
+// 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
+#ifndef MH_SMALL_WAVES
+#define MH_SMALL_WAVES 4
+#endif
+constexpr int kSmallWaves = MH_SMALL_WAVES;  // waves per workgroup (one tile each)
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
@@ -804,7 +809,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   // the table fall outside the descriptor), issued behind the offsets so that the
   // offsets wait below is an exact vmcnt leaving the table loads in flight; the
   // table's L2 round trip overlaps the offsets' HBM one.
-  constexpr int kLutLoads = kLut14Bytes / 16 / (64 * kSmallWaves);  // 4
+  constexpr int kLutLoads = kLut14Bytes / 16 / (64 * kSmallWaves);  // 8
   static_assert(kLut14Bytes == kLutLoads * 16 * 64 * kSmallWaves, "whole table per pass");
   v4u32 L[kLutLoads];
   {
