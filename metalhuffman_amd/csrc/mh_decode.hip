@@ -343,7 +343,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     if (kDelta) {                                                                   \
       if (MH_PERM3) sv[J] = S; else OW = __builtin_amdgcn_perm(S, OW, ins_sel1(J));  \
     } else {                                                                        \
-      OW = __builtin_amdgcn_perm(e + 0x100u, OW, ins_sel1(J));                      \
+      OW = __builtin_amdgcn_perm(e + 0xFFu, OW, ins_sel1(J));  /* byte 1: symbol */  \
     }                                                                               \
   }
 #define MH_STEP(J, OW)                                                              \

@@ -318,3 +318,22 @@ def test_batch_kernel_flat_table(mh, oracle, device):
     for i, im in enumerate(imgs):
         assert np.array_equal(out[i], im), i
     assert np.array_equal(out[3], _oracle_decode(oracle, efs[3]))
+
+
+@pytest.mark.parametrize("prepared", [True, False])
+@pytest.mark.parametrize("flags", [0, 1])
+def test_zero_width_windows_match_reference(mh, oracle, device, prepared, flags):
+    """Windows the table does not decode ({0,0}: the reference's dummy T2 subtable,
+    HuffmanUtil.cpp:550-556) consume nothing and yield symbol 0 -- prev repeats with
+    deltas, the byte is 0 without (AAPLShaders.metal:241-268). A single-symbol
+    alphabet has the one code '0', so all-ones code bytes hit that entry on every
+    lookup; both kernels (prepared table: small-launch; in-kernel table: batch)."""
+    from metalhuffman_amd import codec as C
+    img = np.zeros((24, 40), np.uint8)
+    ef = mh.encode_frame(img, flags=flags)
+    bad = C.EncodedFrame(ef.width, ef.height, ef.canon, np.full_like(ef.codes, 0xFF),
+                         ef.block_offsets, None, ef.flags)
+    out = _decode([bad, bad], device, prepared)
+    ref = _oracle_decode(oracle, bad)
+    assert not ref.any()
+    assert np.array_equal(out[0], ref) and np.array_equal(out[1], ref)
