@@ -18,7 +18,8 @@ event pairs on the launch stream around the same launches issued eagerly right
 after the timed region (HIP does not time events recorded inside a capture).
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU; rank 0 broadcasts the shared T1||T2 table over RCCL (xGMI) once; frames
+per GPU; rank 0 broadcasts the 256-byte canonical header over RCCL (xGMI) once and every
+rank builds T1/T2 and its decode table on its own GPU (mh_build_tables_device); frames
 are sharded (each rank decodes its own), no collective on the data path;
 value = all frames decoded / max-over-ranks wall time ("weak" scaling).
 

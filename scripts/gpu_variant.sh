@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-V=${V:-dyn}
+V=${V:?set V=<variant name>}
 MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$V.so timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_$V.log 2>&1
 rc=$?
 tail -3 gpurun_out/pytest_gpu_$V.log
