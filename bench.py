@@ -194,9 +194,9 @@ def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
 def stream_h2d(efs, tables, device, n_frames=2048, warmup=1024):
     """BASELINE config 5 on one GPU through the native stream (mh_stream_*):
     frames start in pinned host memory; each is copied H2D (codes + block offsets,
-    hipMemcpyAsync on the stream's copy stream) into one of two device slots and
-    decoded by that slot's captured graph on the compute stream, the copy of frame
-    i+1 overlapping the decode of frame i. Reports sustained frames/s and decoded
+    one hipMemcpyAsync) into one of two device slots and decoded by that slot's
+    captured graph, both on the slot's own stream, so the copy of frame i+1 (the
+    other slot) overlaps the decode of frame i. Reports sustained frames/s and decoded
     MB/s including PCIe, and the single-frame latency (submit -> decoded, nothing
     queued). Never the headline `value` (inputs are not resident in HBM)."""
     from metalhuffman_amd.stream import FrameStream, pinned_frame
@@ -234,7 +234,7 @@ def stream_h2d(efs, tables, device, n_frames=2048, warmup=1024):
             "value_MBps_incl_pcie": round(n_frames * W * H / wall / 1e6, 1),
             "h2d_bytes_per_frame": int(h2d), "h2d_GBps": round(n_frames * h2d / wall / 1e9, 2),
             "latency_us_p50": round(lat[len(lat) // 2], 1), "latency_us_max": round(lat[-1], 1),
-            "slots": 2, "launch": "native mh_stream: one H2D DMA per frame on a copy stream + per-slot hipGraph decode"}
+            "slots": 2, "launch": "native mh_stream: per slot one stream, one H2D DMA + a captured hipGraph decode per frame"}
 
 
 def copy_bandwidth(device, nbytes=1 << 30, reps=20):

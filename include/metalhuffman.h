@@ -194,7 +194,7 @@ typedef struct mh_stream mh_stream;
 int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_slots,
                      uint8_t *const *d_outputs, mh_stream **out);
 /* Queue one frame: H2D copy of its host buffers (pinned memory for a DMA) into
- * the next slot once that slot's previous decode is done, then the slot's
+ * the next slot, after that slot's previous decode (same stream), then the slot's
  * decode. codes_bytes includes the MH_CODES_PAD zero bytes; h_block_init must
  * be given iff the stream was created with it. When the host codes follow the
  * block offsets at byte round_up(4*NB, 16) of one buffer, both move in one DMA.
@@ -204,7 +204,11 @@ int mh_stream_submit(mh_stream *s, const uint8_t *h_codes, uint64_t codes_bytes,
                      uint32_t *slot);
 /* The slot's output raster (device); valid until n_slots further submits. */
 uint8_t *mh_stream_output(mh_stream *s, uint32_t slot, size_t *out_pitch);
-/* The stream's compute stream (hipStream_t), for events or dependent work. */
+/* Each slot copies and decodes on its own hipStream_t (stream order keeps a slot's
+ * decode ahead of the copy that reuses it). mh_stream_slot_stream: the stream of
+ * `slot`, for events or work that consumes its raster; mh_stream_compute_stream:
+ * the stream of the most recent submit. */
+void *mh_stream_slot_stream(mh_stream *s, uint32_t slot);
 void *mh_stream_compute_stream(mh_stream *s);
 int mh_stream_wait(mh_stream *s, uint32_t slot);  /* that slot's decode done */
 int mh_stream_synchronize(mh_stream *s);

@@ -24,7 +24,8 @@ EXPORTS = (
     "mh_codes_bound", "mh_encode_huffman", "mh_encode_frame", "mh_canonical_codes",
     "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
     "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
-    "mh_stream_compute_stream", "mh_stream_wait", "mh_stream_synchronize", "mh_stream_destroy",
+    "mh_stream_compute_stream", "mh_stream_slot_stream", "mh_stream_wait", "mh_stream_synchronize",
+    "mh_stream_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
     "mh_container_header", "mh_parse_container_header", "mh_check",
 )
@@ -89,6 +90,8 @@ def lib() -> ctypes.CDLL:
         L.mh_stream_output.restype = _vp
         L.mh_stream_compute_stream.argtypes = [_vp]
         L.mh_stream_compute_stream.restype = _vp
+        L.mh_stream_slot_stream.argtypes = [_vp, ctypes.c_uint32]
+        L.mh_stream_slot_stream.restype = _vp
         L.mh_stream_wait.argtypes = [_vp, ctypes.c_uint32]
         L.mh_stream_synchronize.argtypes = [_vp]
         L.mh_stream_destroy.argtypes = [_vp]

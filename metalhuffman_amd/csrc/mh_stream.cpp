@@ -3,12 +3,16 @@
 // (Shared/AAPLRenderer.m:1178-1921, one decode per drawInMTKView).
 //
 // A stream owns `slots` device slots (codes, block offsets, optional per-block
-// init bytes, output raster). mh_stream_submit copies one frame's host buffers
-// into the next slot on a copy stream (hipMemcpyAsync; pinned host memory makes
-// it a DMA) and replays that slot's captured decode graph on a compute stream,
-// so the copy of frame i+1 overlaps the decode of frame i. A slot is reused only
-// after its previous decode has finished (event wait on the copy stream), and its
-// output stays valid until `slots` further submits.
+// init bytes, output raster), each with its own HIP stream. mh_stream_submit
+// copies one frame's host buffers into the next slot (hipMemcpyAsync; pinned host
+// memory makes it a DMA) and replays that slot's captured decode graph, both on
+// the slot's stream: the copy of frame i+1 (next slot, next stream) overlaps the
+// decode of frame i, and stream order alone keeps a slot's previous decode ahead
+// of the copy that reuses it -- no cross-stream event per frame. (A copy stream
+// plus a compute stream needed an event record and a cross-stream wait at each
+// hand-off and sustained 16.2 K frames/s; per-slot streams 20.8-21.3 K, the rate
+// of bare back-to-back copies: profiles/r01_v17_stream_slots.txt.) A slot's output
+// stays valid until `slots` further submits.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,13 +31,14 @@ struct mh_stream {
     uint8_t *init = nullptr;
     uint8_t *out = nullptr;
     bool own_out = true;
-    hipEvent_t copied = nullptr, done = nullptr;
+    hipEvent_t done = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    hipStream_t stream = nullptr;  // this slot's copies + decode, in order
     bool used = false;
   };
   int device = 0;
-  hipStream_t copy = nullptr, compute = nullptr;
+  uint32_t last = 0;  // slot of the most recent submit
   mh_frame proto{};
   uint64_t cap = 0;
   uint64_t nb = 0;
@@ -51,24 +56,22 @@ void release(mh_stream *s) {
   for (auto &sl : s->slots) {
     if (sl.exec) (void)hipGraphExecDestroy(sl.exec);
     if (sl.graph) (void)hipGraphDestroy(sl.graph);
-    if (sl.copied) (void)hipEventDestroy(sl.copied);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.stream) (void)hipStreamDestroy(sl.stream);
     (void)hipFree(sl.base);
     (void)hipFree(sl.init);
     if (sl.own_out) (void)hipFree(sl.out);
   }
-  if (s->copy) (void)hipStreamDestroy(s->copy);
-  if (s->compute) (void)hipStreamDestroy(s->compute);
   delete s;
 }
 
-bool decode_slot(mh_stream *s, mh_stream::Slot &sl) {
+bool decode_slot(mh_stream *s, mh_stream::Slot &sl, hipStream_t st) {
   mh_frame f = s->proto;
   f.d_codes = sl.codes;
   f.codes_bytes = s->cap;
   f.d_block_offsets = sl.offsets;
   f.d_block_init = sl.init;
-  return mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute) == MH_OK;
+  return mh_decode(&f, sl.out, s->pitch, s->out_bytes, st) == MH_OK;
 }
 
 }  // namespace
@@ -101,10 +104,7 @@ int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_
   const char *ge = std::getenv("MH_STREAM_GRAPHS");
   s->graphs = !(ge && ge[0] == '0');
   int rc = MH_OK;
-  if (hipGetDevice(&s->device) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->compute, hipStreamNonBlocking) != hipSuccess)
-    rc = MH_ERR_HIP;
+  if (hipGetDevice(&s->device) != hipSuccess) rc = MH_ERR_HIP;
   for (uint32_t i = 0; i < n_slots && rc == MH_OK; ++i) {
     mh_stream::Slot &sl = s->slots[i];
     if (d_outputs) {
@@ -119,8 +119,8 @@ int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_
         (want_init && hipMalloc(&sl.init, s->nb) != hipSuccess) ||
         (!d_outputs && hipMalloc(&sl.out, s->out_bytes) != hipSuccess) ||
         hipMemset(sl.base, 0, s->off_bytes + s->cap) != hipSuccess ||
-        hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
       rc = MH_ERR_HIP;
       break;
     }
@@ -140,19 +140,20 @@ int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_
     f.d_block_init = sl.init;
     // one eager decode first: validates the arguments and caches the launch
     // geometry queries outside the capture
-    const int wrc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute);
+    hipStream_t cs = sl.stream;
+    const int wrc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, cs);
     if (wrc != MH_OK) {
       rc = wrc;
       break;
     }
     if (!s->graphs) continue;
-    if (hipStreamBeginCapture(s->compute, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
       rc = MH_ERR_HIP;
       break;
     }
-    const int drc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, s->compute);
+    const int drc = mh_decode(&f, sl.out, s->pitch, s->out_bytes, cs);
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(s->compute, &g);
+    const hipError_t e = hipStreamEndCapture(cs, &g);
     sl.graph = g;
     if (drc != MH_OK || e != hipSuccess) {
       rc = drc != MH_OK ? drc : MH_ERR_HIP;
@@ -180,25 +181,23 @@ int mh_stream_submit(mh_stream *s, const uint8_t *h_codes, uint64_t codes_bytes,
   if (!h_block_init != !s->slots[0].init) return MH_ERR_INVALID_ARG;
   const uint32_t k = s->next;
   mh_stream::Slot &sl = s->slots[k];
-  // the slot's previous decode must be done before its buffers are overwritten
-  if (sl.used && hipStreamWaitEvent(s->copy, sl.done, 0) != hipSuccess) return MH_ERR_HIP;
-  // host offsets and codes laid out like the slot ([offsets, padded to 16 B][codes]):
+  // copy then decode on the slot's own stream (its previous decode is ahead in it).
+  // Host offsets and codes laid out like the slot ([offsets, padded to 16 B][codes]):
   // one DMA; otherwise two
   const bool packed = h_codes == reinterpret_cast<const uint8_t *>(h_block_offsets) + s->off_bytes;
   if ((packed ? hipMemcpyAsync(sl.base, h_block_offsets, s->off_bytes + codes_bytes,
-                               hipMemcpyHostToDevice, s->copy) != hipSuccess
-              : (hipMemcpyAsync(sl.codes, h_codes, codes_bytes, hipMemcpyHostToDevice, s->copy) !=
+                               hipMemcpyHostToDevice, sl.stream) != hipSuccess
+              : (hipMemcpyAsync(sl.codes, h_codes, codes_bytes, hipMemcpyHostToDevice, sl.stream) !=
                      hipSuccess ||
                  hipMemcpyAsync(sl.offsets, h_block_offsets, s->nb * 4, hipMemcpyHostToDevice,
-                                s->copy) != hipSuccess)) ||
+                                sl.stream) != hipSuccess)) ||
       (h_block_init &&
-       hipMemcpyAsync(sl.init, h_block_init, s->nb, hipMemcpyHostToDevice, s->copy) != hipSuccess) ||
-      hipEventRecord(sl.copied, s->copy) != hipSuccess ||
-      hipStreamWaitEvent(s->compute, sl.copied, 0) != hipSuccess ||
-      (s->graphs ? hipGraphLaunch(sl.exec, s->compute) != hipSuccess : !decode_slot(s, sl)) ||
-      hipEventRecord(sl.done, s->compute) != hipSuccess)
+       hipMemcpyAsync(sl.init, h_block_init, s->nb, hipMemcpyHostToDevice, sl.stream) != hipSuccess) ||
+      (s->graphs ? hipGraphLaunch(sl.exec, sl.stream) != hipSuccess : !decode_slot(s, sl, sl.stream)) ||
+      hipEventRecord(sl.done, sl.stream) != hipSuccess)
     return MH_ERR_HIP;
   sl.used = true;
+  s->last = k;
   s->next = (k + 1) % (uint32_t)s->slots.size();
   if (slot_out) *slot_out = k;
   return MH_OK;
@@ -210,7 +209,11 @@ uint8_t *mh_stream_output(mh_stream *s, uint32_t slot, size_t *out_pitch) {
   return s->slots[slot].out;
 }
 
-void *mh_stream_compute_stream(mh_stream *s) { return s ? (void *)s->compute : nullptr; }
+void *mh_stream_compute_stream(mh_stream *s) { return s ? (void *)s->slots[s->last].stream : nullptr; }
+
+void *mh_stream_slot_stream(mh_stream *s, uint32_t slot) {
+  return (s && slot < s->slots.size()) ? (void *)s->slots[slot].stream : nullptr;
+}
 
 int mh_stream_wait(mh_stream *s, uint32_t slot) {
   if (!s || slot >= s->slots.size()) return MH_ERR_INVALID_ARG;
@@ -220,9 +223,9 @@ int mh_stream_wait(mh_stream *s, uint32_t slot) {
 
 int mh_stream_synchronize(mh_stream *s) {
   if (!s) return MH_ERR_INVALID_ARG;
-  return (hipStreamSynchronize(s->copy) == hipSuccess && hipStreamSynchronize(s->compute) == hipSuccess)
-             ? MH_OK
-             : MH_ERR_HIP;
+  for (auto &sl : s->slots)
+    if (sl.stream && hipStreamSynchronize(sl.stream) != hipSuccess) return MH_ERR_HIP;
+  return MH_OK;
 }
 
 int mh_stream_destroy(mh_stream *s) {

@@ -1,6 +1,6 @@
 """Frames streamed from host memory (BASELINE config 5): a thin wrapper over the
-native mh_stream_* API (csrc/mh_stream.cpp) -- per-slot device buffers, an H2D copy
-stream, a compute stream, one captured decode graph per slot -- mirroring the
+native mh_stream_* API (csrc/mh_stream.cpp) -- per-slot device buffers, one HIP
+stream and one captured decode graph per slot (copy then decode in stream order) -- mirroring the
 reference's per-frame command buffer (Shared/AAPLRenderer.m:1178-1921)."""
 from __future__ import annotations
 
@@ -51,6 +51,10 @@ class FrameStream:
     def output(self, slot: int) -> torch.Tensor:
         """[H, pitch] raster of `slot` (valid until `slots` further submits)."""
         return self.outputs[slot]
+
+    def slot_stream(self, slot: int) -> int:
+        """hipStream_t of `slot` (its copy and decode run there, in order)."""
+        return int(N.lib().mh_stream_slot_stream(self._h, slot) or 0)
 
     def wait(self, slot: int) -> None:
         N.check(N.lib().mh_stream_wait(self._h, slot), "mh_stream_wait")

@@ -15,7 +15,7 @@ t1, t2 = efs[0].tables()
 tabs = D.DeviceTables.upload(t1, t2, dev)
 hosts = [pinned_frame(ef) for ef in efs]
 nbytes = int(np.mean([ef.codes.size + 4 * ef.n_blocks for ef in efs]))
-for slots in (2, 3, 4, 8):
+for slots in (2, 4):
     fs = FrameStream(tabs, 2048, 1536, max(ef.codes.size for ef in efs), slots=slots, device=dev)
     for rnd in range(3):
         n = 1024
