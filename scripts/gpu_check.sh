@@ -11,9 +11,12 @@ echo "smoke ok"
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 : > gpurun_out/ktrace_summary.txt
-for wl in frame batch tile8192 tile8192_random; do
+# same steps / warm-up as the bench line each number is compared with (the frame
+# headline: 200 / 20; the extras: bench.py's own counts)
+for spec in frame:200:20 batch:256:256 tile8192:512:512 tile8192_random:512:512; do
+  IFS=: read wl k w <<< "$spec"
   rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_$wl
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }
-  { echo "== bench.py --workload $wl (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl; } >> gpurun_out/ktrace_summary.txt
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --steps $k --warmup $w --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }
+  { echo "== bench.py --workload $wl --steps $k --warmup $w (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl $k; } >> gpurun_out/ktrace_summary.txt
 done
 cat gpurun_out/ktrace_summary.txt
