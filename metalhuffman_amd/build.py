@@ -115,7 +115,7 @@ def build_probe(force: bool = False, verbose: bool = False) -> str:
     """The achievable-HBM probe bench.py reports beside the roofline (measurement
     infrastructure, not the decoder): scripts/micro/libhbm_probe.so."""
     if force or _stale(PROBE_LIB, [PROBE_SRC]):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-Wno-unused-result",
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared",
                "-o", PROBE_LIB, PROBE_SRC]
         if verbose:
             print(" ".join(cmd), flush=True)

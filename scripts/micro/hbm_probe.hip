@@ -61,17 +61,17 @@ int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
   if (hipMalloc(&src, src_bytes) != hipSuccess || hipMalloc(&dst, dst_bytes) != hipSuccess ||
       hipMalloc(&sink, 4) != hipSuccess)
     return -2;
-  hipMemset(src, 1, src_bytes);
+  (void)hipMemset(src, 1, src_bytes);
   int dev = 0, cus = 0;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const dim3 grid(cus * 16), block(256);
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   float best = 1e30f;
   for (int r = 0; r < reps + 1; ++r) {
-    hipEventRecord(e0, 0);
+    (void)hipEventRecord(e0, 0);
     const v4u *s = (const v4u *)src;
     v4u *d = (v4u *)dst;
     switch (mode + (nt ? 0 : 10)) {
@@ -83,20 +83,20 @@ int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
       case 12: hipLaunchKernelGGL((stream_kernel<2, false>), grid, block, 0, 0, s, d, n_units, sink); break;
       default: hipLaunchKernelGGL((stream_kernel<3, false>), grid, block, 0, 0, s, d, n_units, sink); break;
     }
-    hipEventRecord(e1, 0);
-    hipEventSynchronize(e1);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
     if (r > 0 && ms < best) best = ms;  // first launch warms up
   }
   const double moved = mode == 1 ? (double)src_bytes : mode == 2 ? (double)dst_bytes
                                                                   : (double)(src_bytes + dst_bytes);
   *gbps = moved / (best * 1e-3) / 1e9;
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(src);
-  hipFree(dst);
-  hipFree(sink);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipFree(sink);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
