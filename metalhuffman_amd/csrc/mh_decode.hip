@@ -359,6 +359,9 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     lo = c ? nw : lo;                                                               \
     const uint32_t d = c ? 4u : 0u;                                                 \
     wa += d;                                                                        \
+    /* swizzled stage: keep wa one register (else it is re-derived as a sum of */  \
+    /* every step's d inside each masked refill, which spills)                */  \
+    if constexpr (Cfg::kSwz) asm volatile("" : "+v"(wa));                          \
     S += d * 8u;                                                                    \
     if constexpr (!Cfg::kMasked) nw = rd(wa + 8);                                   \
   }
