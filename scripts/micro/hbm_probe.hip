@@ -5,6 +5,8 @@
 //   mode 3 the decoder's mix: read 2 vectors, write 3 (2.12 MB read : 3.15 MB written per
 //          2048x1536 frame is 0.67; 2:3 is the nearest whole-vector ratio);
 //   modes 4-6: copy, write-only and the mix with default-policy (not nt) stores.
+// Loads are non-temporal too. Each mode reports the best of grids of 2, 4 and 16
+// workgroups per CU (scripts/micro/hbm_sweep.hip: the mix peaks at 2-4 per CU).
 // Built by metalhuffman_amd.build.build_probe() into scripts/micro/libhbm_probe.so.
 #include <hip/hip_runtime.h>
 
@@ -28,14 +30,14 @@ __global__ void __launch_bounds__(256) stream_kernel(const v4u *__restrict__ src
   v4u acc = {0, 0, 0, 0};
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_units; i += stride) {
     if (kMode == 0) {
-      st<kNt>(src[i], &dst[i]);
+      st<kNt>(__builtin_nontemporal_load(&src[i]), &dst[i]);
     } else if (kMode == 1) {
-      acc ^= src[i];
+      acc ^= __builtin_nontemporal_load(&src[i]);
     } else if (kMode == 2) {
       v4u v = {(unsigned)i, 1u, 2u, 3u};
       st<kNt>(v, &dst[i]);
     } else {  // unit = 2 vectors read, 3 written, each stream coalesced
-      const v4u a = src[i], b = src[n_units + i];
+      const v4u a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[n_units + i]);
       st<kNt>(a, &dst[i]);
       st<kNt>(b, &dst[n_units + i]);
       st<kNt>(a ^ b, &dst[2 * n_units + i]);
@@ -65,12 +67,13 @@ int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const dim3 grid(cus * 16), block(256);
+  const dim3 block(256);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   float best = 1e30f;
-  for (int r = 0; r < reps + 1; ++r) {
+  for (int r = 0; r < 3 * (reps + 1); ++r) {
+    const dim3 grid(cus * (r % 3 == 0 ? 2 : r % 3 == 1 ? 4 : 16));
     (void)hipEventRecord(e0, 0);
     const v4u *s = (const v4u *)src;
     v4u *d = (v4u *)dst;
@@ -87,7 +90,7 @@ int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    if (r > 0 && ms < best) best = ms;  // first launch warms up
+    if (r >= 3 && ms < best) best = ms;  // the first launch of each grid warms up
   }
   const double moved = mode == 1 ? (double)src_bytes : mode == 2 ? (double)dst_bytes
                                                                   : (double)(src_bytes + dst_bytes);
