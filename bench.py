@@ -281,8 +281,10 @@ def hbm_probe(nbytes=1 << 30, reps=10):
 
 
 def encode_rate(device, bb, reps=32):
-    """The producer side: GPU encoder (mh_encode_frame_device: one host sync for the
-    histogram per frame) vs the host codec (mh_encode_frame, one thread), both on
+    """The producer side: GPU encoder, synchronous (mh_encode_frame_device: one host
+    sync per frame for the header and byte count) and device-only
+    (mh_encode_frame_device_async: the Huffman tree on the device, frames enqueued
+    back to back), vs the host codec (mh_encode_frame, one thread), all on
     BigBridge-shuffled frames, wall clock per frame."""
     import metalhuffman_amd as mh
     from metalhuffman_amd import frames as F
@@ -290,8 +292,10 @@ def encode_rate(device, bb, reps=32):
     imgs = [F.block_shuffle(bb, 900 + k) for k in range(4)]
     dimgs = [torch.from_numpy(im).to(device) for im in imgs]
     enc = Encoder(bb.shape[1], bb.shape[0], device)
+    codes = [torch.empty(enc.cap, dtype=torch.uint8, device=device) for _ in range(4)]
     for k in range(4):
         enc.encode(dimgs[k])
+        enc.encode_async(dimgs[k], codes=codes[k])
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for k in range(reps):
@@ -299,10 +303,17 @@ def encode_rate(device, bb, reps=32):
     torch.cuda.synchronize(device)
     gpu_s = (time.perf_counter() - t0) / reps
     t0 = time.perf_counter()
+    for k in range(reps):
+        enc.encode_async(dimgs[k % 4], codes=codes[k % 4])
+    torch.cuda.synchronize(device)
+    async_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
     for k in range(4):
         mh.encode_frame(imgs[k])
     cpu_s = (time.perf_counter() - t0) / 4
     return {"gpu_ms_per_frame": round(gpu_s * 1e3, 3), "gpu_MBps": round(bb.size / gpu_s / 1e6, 1),
+            "gpu_async_ms_per_frame": round(async_s * 1e3, 3),
+            "gpu_async_MBps": round(bb.size / async_s / 1e6, 1),
             "host_1thread_ms_per_frame": round(cpu_s * 1e3, 2), "host_1thread_MBps": round(bb.size / cpu_s / 1e6, 1)}
 
 

@@ -161,18 +161,34 @@ int mh_build_tables_device(const uint8_t *d_canon_header, mh_lookup_symbol *d_ta
 /* mh_encode_frame: HuffmanEncoder.cpp:310-381, HuffmanUtil.cpp:1051-1131,  */
 /* AAPLRenderer.m:374-688).                                                 */
 
-/* Device workspace mh_encode_frame_device needs for a width x height frame. */
+/* Device workspace mh_encode_frame_device / _async need for a width x height
+ * frame (the larger figure, the synchronous call's). */
 size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height);
 
-/* Encode the device frame d_gray (W x H bytes, row stride W): block split,
- * deltas (unless MH_FLAG_NO_DELTA) and histogram on the device, the Huffman
- * tree on the host from the 256 counts, then canonical codes, block offsets (a
- * prefix sum of per-block bit lengths) and MSB-first bit packing on the device.
- * Writes canon_header (host), d_codes (4-byte aligned; *codes_len = payload +
- * MH_CODES_PAD zero bytes, codes_cap >= round_up(*codes_len, 4)),
- * d_block_offsets (u32[NB]) and, if non-NULL, d_block_init (u8[NB], the
- * IMPL_DELTAS_AND_INIT_ZERO_DELTA variant). d_workspace: 256-byte aligned,
- * mh_encode_workspace_bytes(). Synchronises `stream` once (the histogram). */
+/* Encode the device frame d_gray (W x H bytes, row stride W) without a host
+ * synchronisation: block split, deltas (unless MH_FLAG_NO_DELTA) and histogram,
+ * the reference's Huffman tree (HuffmanEncoder.cpp:29-145, same tie-breaking as
+ * mh_code_lengths) and canonical codes on one workgroup, block offsets (a prefix
+ * sum of per-block bit lengths) and MSB-first bit packing, all on `stream`.
+ * Writes d_canon_header (device u8[256]), d_codes (4-byte aligned; the byte
+ * count is payload + MH_CODES_PAD zero bytes), *d_codes_len (device u64,
+ * optional), d_block_offsets (u32[NB]) and, if non-NULL, d_block_init (u8[NB],
+ * the IMPL_DELTAS_AND_INIT_ZERO_DELTA variant). *d_status (device int32,
+ * optional) becomes MH_OK, MH_ERR_EMPTY, MH_ERR_CODE_TOO_LONG (depth > 16) or
+ * MH_ERR_CAPACITY (round_up(codes_len, 4) > codes_cap, or >= 2^32 code bits);
+ * on an error no code bytes or offsets are written and *d_codes_len is 0.
+ * d_workspace: 256-byte aligned, mh_encode_workspace_bytes(). The return value
+ * covers only argument checks and launch errors. A frame encoded this way goes to
+ * mh_build_tables_device (the header) and mh_decode without touching the host. */
+int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
+                                 uint8_t *d_canon_header, uint8_t *d_codes, uint64_t codes_cap,
+                                 uint64_t *d_codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                                 int32_t *d_status, void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* mh_encode_frame_device_async, then one copy and one synchronisation of
+ * `stream` to return canon_header and *codes_len on the host; the device status
+ * becomes the return value (output byte-identical to mh_encode_frame:
+ * HuffmanEncoder.cpp:310-381, HuffmanUtil.cpp:1051-1131, AAPLRenderer.m:374-688). */
 int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
                            uint8_t canon_header[256], uint8_t *d_codes, uint64_t codes_cap,
                            uint64_t *codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,

@@ -27,6 +27,7 @@ EXPORTS = (
     "mh_stream_compute_stream", "mh_stream_slot_stream", "mh_stream_wait", "mh_stream_synchronize",
     "mh_stream_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
+    "mh_encode_frame_device_async",
     "mh_container_header", "mh_parse_container_header", "mh_check",
 )
 
@@ -103,6 +104,9 @@ def lib() -> ctypes.CDLL:
         L.mh_encode_frame_device.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
                                              _vp, ctypes.c_uint64, _u64p, _vp, _vp, _vp, ctypes.c_size_t,
                                              _vp]
+        L.mh_encode_frame_device_async.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                   _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
+                                                   ctypes.c_size_t, _vp]
         L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint8, _u8p, ctypes.c_size_t]
         L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

@@ -4,28 +4,33 @@
 //   split + deltas   Shared/Util.m:233-323, Shared/AAPLRenderer.m:432-515 (one thread
 //                    per 8x8 block, zero padding past W/H, optional init byte :449-473)
 //   histogram        HuffmanEncoder.cpp:310-330 (symbol counts; LDS then global atomics)
-//   code lengths     HuffmanEncoder.cpp:29-145 -- on the HOST from the 256 counts (the
-//                    reference's node-array tie-breaking is inherently sequential and
-//                    tiny), mh_code_lengths + canonical codes huff_util.hpp:94-193
+//   code lengths     HuffmanEncoder.cpp:29-145 -- on the device (enc_tree_kernel): the
+//                    reference's sorted node array with upper_bound insertion is the
+//                    two-queue Huffman merge with ties going to the leaf queue; then
+//                    canonical codes huff_util.hpp:94-193 and the code byte count
 //   block offsets    HuffmanUtil.cpp:1103-1128 -- an exclusive prefix sum of the
 //                    per-block code-length sums
 //   bit packing      HuffmanEncoder.cpp:211-381 -- MSB-first; each block writes its own
 //                    words, OR-ing the two it may share with its neighbours
-// The call synchronises its stream once (the 1 KB histogram comes to the host).
+// mh_encode_frame_device_async never synchronises (header, code bytes and status are
+// written to device memory); mh_encode_frame_device runs it and synchronises once at
+// the end to return the header and the byte count on the host.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include "../../include/metalhuffman.h"
 
-extern "C" int mh_code_lengths(const uint64_t freq[256], uint8_t canon_header[256]);
-extern "C" int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]);
 
 namespace {
 
 constexpr uint32_t kScanTile = 1024;  // blocks per workgroup in the offsets scan
+constexpr uint32_t kResultBytes = 512;  // mh_encode_frame_device: header, byte count, status
+constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
+constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
 
 struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint8_t *sym;       // nb * 64 block symbols
@@ -33,6 +38,7 @@ struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint32_t *tsum;     // ceil(nb / kScanTile) tile sums (then tile offsets)
   uint64_t *hist;     // 256 counts
   uint32_t *table;    // 256 x (code_lj16 << 16 | len)
+  uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits]]
 };
 
 constexpr uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -50,181 +56,436 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   o += align256(256 * 8);
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
+  if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
+  o += align256((kTotalBits + 1) * 8);
   return o;
 }
 
-// One thread per block: pixels -> 64 symbols (block order, row-major inside the
-// block, zero past the frame edge), per-block deltas, histogram.
+// Eight lanes per block, one 8-pixel block row each (lane = 8 * block + row), so a
+// wave reads 8 image rows x 64 contiguous bytes and writes 512 contiguous symbol
+// bytes. Pixels -> symbols (block order, row-major inside the block, zero past the
+// frame edge), per-block deltas in SWAR with the previous pixel from the lane one
+// row up, histogram into 16 replicated LDS copies (BigBridge-like deltas are mostly
+// one symbol; one copy would serialise every atomic on it). Grid-stride over groups
+// of 32 blocks; one global atomic per used bin per workgroup.
+constexpr uint32_t kHistCopies = 16;
+#ifndef MH_SPLIT_WGS  // split workgroups: each adds one global atomic per used bin
+#define MH_SPLIT_WGS 256
+#endif
+#ifndef MH_TREE_STAMPS
+#define MH_TREE_STAMPS 0
+#endif
+
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
-                                                        uint8_t *sym, uint8_t *block_init,
+                                                        uint32_t vec, uint8_t *sym, uint8_t *block_init,
                                                         uint64_t *hist) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+  __shared__ uint32_t h[256 * kHistCopies];
+  for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
   __syncthreads();
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < nb) {
-    const uint32_t bx = (uint32_t)(b % bw), by = (uint32_t)(b / bw);
-    uint8_t v[64];
-    for (uint32_t r = 0; r < 8; ++r) {
-      const uint32_t y = by * 8 + r;
-      for (uint32_t c = 0; c < 8; ++c) {
-        const uint32_t x = bx * 8 + c;
-        v[r * 8 + c] = (y < H && x < W) ? gray[(uint64_t)y * W + x] : 0;
+  const uint32_t r = threadIdx.x & 7u;
+  const uint32_t copy = threadIdx.x % kHistCopies;
+  const bool delta = !(flags & MH_FLAG_NO_DELTA);
+  for (uint64_t g = blockIdx.x; g * 32 < nb; g += gridDim.x) {
+    const uint64_t b = g * 32 + (threadIdx.x >> 3);
+    const bool on = b < nb;
+    const uint32_t bx = on ? (uint32_t)(b % bw) : 0u, by = on ? (uint32_t)(b / bw) : 0u;
+    const uint32_t y = by * 8 + r;
+    uint64_t q = 0;
+    if (on && y < H) {
+      const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
+      if (vec) {  // W % 8 == 0 and an 8-byte aligned frame: every block row is inside
+        q = *reinterpret_cast<const uint64_t *>(row);
+      } else {
+        for (uint32_t c = 0; c < 8; ++c)
+          if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
       }
     }
-    if (!(flags & MH_FLAG_NO_DELTA)) {
-      uint8_t prev = 0;
-      for (int i = 0; i < 64; ++i) {
-        const uint8_t cur = v[i];
-        v[i] = (uint8_t)(cur - prev);
-        prev = cur;
+    uint64_t v = q;
+    if (delta) {
+      // previous pixel: the last pixel of the row above in the same block, 0 for row 0
+      const uint32_t up = (uint32_t)__shfl_up((uint32_t)(q >> 56), 1);
+      const uint64_t p = (q << 8) | (r ? up : 0u);
+      constexpr uint64_t kH = 0x8080808080808080ull;
+      v = ((q | kH) - (p & ~kH)) ^ ((q ^ ~p) & kH);  // bytewise q - p
+      if (block_init && r == 0 && on) {
+        block_init[b] = (uint8_t)v;
+        v &= ~0xFFull;
       }
-      if (block_init) {
-        block_init[b] = v[0];
-        v[0] = 0;
-      }
-    } else if (block_init) {
+    } else if (block_init && r == 0 && on) {
       block_init[b] = 0;
     }
-    uint64_t *dst = reinterpret_cast<uint64_t *>(sym + b * 64);
-    for (int k = 0; k < 8; ++k) {
-      uint64_t q = 0;
-      for (int j = 0; j < 8; ++j) q |= (uint64_t)v[k * 8 + j] << (8 * j);
-      dst[k] = q;
+    if (on) {
+      reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
+      for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
     }
-    for (int i = 0; i < 64; ++i) atomicAdd(&h[v[i]], 1u);
   }
   __syncthreads();
-  if (h[threadIdx.x]) atomicAdd((unsigned long long *)&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+  uint32_t c = 0;
+  for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
+  if (c) atomicAdd((unsigned long long *)&hist[threadIdx.x], (unsigned long long)c);
 }
 
-// Per-block code-length sums.
-__global__ void __launch_bounds__(256) enc_blen_kernel(const uint8_t *sym, const uint32_t *table,
-                                                       uint64_t nb, uint32_t *blen) {
+// One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
+// from the 256 counts. The reference keeps every node in one array sorted by weight,
+// inserts at upper_bound (a new node goes after all nodes of equal weight) and merges
+// the two front-most entries. Leaves enter first, in symbol order, so they sit sorted
+// by (weight, symbol); merged weights never decrease, so internal nodes sit in
+// creation order after every leaf of equal weight. That is the two-queue merge
+// (sorted leaves, internal nodes in creation order) taking the leaf on a tie: the
+// same tree, in O(n). The merge is serial (one lane, queue fronts in registers, one
+// LDS round trip per merge); leaf ranks, depths (pointer jumping over the parent
+// links: 9 rounds cover 511 nodes) and canonical ranks (ballots) are parallel. Then
+// the canonical codes
+// (huff_util.hpp:94-193), the code table, the code byte count and the status
+// (mh_code_lengths' errors, the caller's capacity).
+__global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uint8_t *canon_out,
+                                                       uint32_t *table, uint64_t *meta, uint64_t *codes_len_out,
+                                                       uint64_t codes_cap, int32_t *status) {
+  constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
+#if MH_TREE_STAMPS  // phase timestamps (s_memtime) into meta[2..] for scripts/enc_profile.py
+#define MH_TREE_STAMP(k) \
+  if (tid == 0) meta[2 + (k)] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) meta[2] = __builtin_amdgcn_s_memtime();
+#else
+#define MH_TREE_STAMP(k)
+#endif
+  __shared__ uint32_t s_lw[258], s_iw[258];
+  __shared__ __attribute__((aligned(16))) uint64_t s_key[256];
+  __shared__ uint32_t s_leaf_sym[256], s_len[256], s_par[2][512], s_dep[2][512];
+  __shared__ uint32_t s_wcnt[4][17], s_first[17], s_n, s_bad;
+  __shared__ unsigned long long s_total;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t f = hist[tid];
+  s_len[tid] = 0;
+  s_lw[tid] = kEnd;
+  s_iw[tid] = kEnd;
+  if (tid < 2) s_lw[256 + tid] = s_iw[256 + tid] = kEnd;
+  if (tid == 0) {
+    s_n = 0;
+    s_bad = 0;
+    s_total = 0;
+  }
+  __syncthreads();
+  MH_TREE_STAMP(1);
+  {
+    // rank of this leaf in (weight, symbol) order: count the smaller keys among all
+    // 256 (16-byte broadcast reads, one 64-bit compare per key). Absent symbols
+    // have key 0, below every present one: subtract their count afterwards.
+    const uint64_t key = f ? (f << 8) | tid : 0;
+    s_key[tid] = key;
+    const uint32_t present = (uint32_t)__syncthreads_count(f != 0);
+    uint32_t below = 0;
+    const ulonglong2 *kv = reinterpret_cast<const ulonglong2 *>(s_key);
+#pragma unroll 16
+    for (uint32_t t = 0; t < 128; ++t) {  // same address across the wave: broadcast reads
+      const ulonglong2 v = kv[t];
+      below += v.x < key ? 1u : 0u;
+      below += v.y < key ? 1u : 0u;
+    }
+    if (f) {
+      const uint32_t rank = below - (256u - present);
+      s_leaf_sym[rank] = tid;
+      s_lw[rank] = (uint32_t)f;
+    }
+    if (tid == 0) s_n = present;
+  }
+  __syncthreads();
+  MH_TREE_STAMP(2);
+  const uint32_t n = s_n;
+  const uint32_t nodes = n ? 2 * n - 1 : 0, root = nodes - 1;
+  if (n >= 2 && tid == 0) {
+    // two-queue merge on one lane, branch-free. Both fronts and both second entries
+    // stay in registers, so a merge's two picks compare registers only; the four
+    // loads that refill them are independent and issued together: one LDS latency
+    // per merge on the serial chain. Weights are u32: a non-root weight is below
+    // the padded pixel count <= 2^32. Empty queue slots hold kEnd (0xFFFFFFFF) and
+    // a tie goes to the leaf, which stays exact even at 2^32 pixels: a real weight
+    // of 2^32 - 1 leaves exactly one other node, a leaf of weight 1, so an empty
+    // leaf queue never meets it. One wave issues one instruction per 4 clocks, so
+    // the loop is kept short (sentinels instead of queue-length checks).
+    uint32_t li = 0, ii = 0, ni = 0;
+    uint32_t l0 = s_lw[0], l1 = s_lw[1], i0 = kEnd, i1 = kEnd;
+    for (uint32_t m = 0; m + 1 < n; ++m) {
+      const bool a_leaf = l0 <= i0;
+      const uint32_t wa = a_leaf ? l0 : i0;
+      const uint32_t ida = a_leaf ? li : n + ii;
+      const uint32_t bl = a_leaf ? l1 : l0, bi = a_leaf ? i0 : i1;  // fronts after pick a
+      const bool b_leaf = bl <= bi;
+      const uint32_t wb = b_leaf ? bl : bi;
+      const uint32_t nl = (a_leaf ? 1u : 0u) + (b_leaf ? 1u : 0u);
+      const uint32_t idb = b_leaf ? li + nl - 1u : n + ii + 1u - nl;
+      s_iw[ni] = wa + wb;  // before the refill loads: LDS keeps program order
+      s_par[0][ida] = n + ni;
+      s_par[0][idb] = n + ni;
+      li += nl;
+      ii += 2u - nl;
+      ++ni;
+      l0 = s_lw[li];
+      l1 = s_lw[li + 1];
+      i0 = s_iw[ii];
+      i1 = s_iw[ii + 1];
+    }
+  }
+  __syncthreads();
+  MH_TREE_STAMP(3);
+  // depths by pointer jumping: dep = 1 + dep(parent) over parent links, root 0
+  for (uint32_t i = tid; i < nodes; i += 256) {
+    s_dep[0][i] = i == root ? 0u : 1u;
+    if (i == root) s_par[0][i] = root;
+  }
+  __syncthreads();
+  MH_TREE_STAMP(4);
+  uint32_t cur = 0;
+  for (uint32_t step = 0; step < 9; ++step) {
+    for (uint32_t i = tid; i < nodes; i += 256) {
+      const uint32_t p = s_par[cur][i];
+      s_dep[cur ^ 1][i] = s_dep[cur][i] + s_dep[cur][p];
+      s_par[cur ^ 1][i] = s_par[cur][p];
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (n == 0) {
+    if (tid == 0) s_bad = (uint32_t)-MH_ERR_EMPTY;
+  } else if (n == 1) {  // single symbol -> 1-bit code "0" (HuffmanEncoder.cpp:118-121)
+    if (tid == 0) s_len[s_leaf_sym[0]] = 1;
+  } else if (tid < n) {
+    const uint32_t d = s_dep[cur][tid];
+    if (d > 16) s_bad = (uint32_t)-MH_ERR_CODE_TOO_LONG;
+    s_len[s_leaf_sym[tid]] = min(d, 255u);
+  }
+  __syncthreads();
+  MH_TREE_STAMP(5);
+  const uint32_t L = s_len[tid];
+  canon_out[tid] = (uint8_t)L;
+  // codes per length and each symbol's rank among equal lengths (symbol order):
+  // one ballot per length per wave, per-wave counts through LDS
+  const uint32_t wave = tid >> 6, lane = tid & 63u;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t in_wave = 0;
+  for (uint32_t l = 1; l <= 16; ++l) {
+    const uint64_t m = __ballot(L == l);
+    if (L == l) in_wave = (uint32_t)__popcll(m & below);
+    if (lane == 0) s_wcnt[wave][l] = (uint32_t)__popcll(m);
+  }
+  uint64_t bits = f * L;  // sum of count x length: wave reduction, one LDS atomic per wave
+  for (int o = 32; o; o >>= 1) bits += __shfl_xor(bits, o);
+  if (lane == 0) atomicAdd(&s_total, (unsigned long long)bits);
+  __syncthreads();
+  MH_TREE_STAMP(6);
+  if (tid == 0) {
+    uint32_t code = 0;  // first code of each length: shift left across every length step
+    for (uint32_t l = 1; l <= 16; ++l) {
+      s_first[l] = code;
+      code = (code + s_wcnt[0][l] + s_wcnt[1][l] + s_wcnt[2][l] + s_wcnt[3][l]) << 1;
+    }
+  }
+  __syncthreads();
+  MH_TREE_STAMP(7);
+  uint32_t e = 0;
+  if (L && L <= 16) {
+    uint32_t rank = in_wave;  // symbols of the same length before this one
+    for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
+    e = ((((s_first[L] + rank) << (16 - L)) & 0xFFFFu) << 16) | L;
+  }
+  table[tid] = e;
+  if (tid == 0) {
+    const uint64_t total = s_total;
+    const uint64_t len = (total + 7) / 8 + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
+    uint32_t bad = s_bad;
+    if (!bad && (total >= (1ull << 32) || ((len + 3) & ~3ull) > codes_cap)) bad = (uint32_t)-MH_ERR_CAPACITY;
+    meta[0] = bad ? 0 : len;
+    meta[1] = bad ? 0 : 1;
+    meta[kTicket] = 0;
+    meta[kTotalBits] = total;
+    if (codes_len_out) *codes_len_out = bad ? 0 : len;
+    if (status) *status = bad ? -(int32_t)bad : MH_OK;
+  }
+  MH_TREE_STAMP(8);
+}
+
+// Block offsets, one kernel: each workgroup zeroes its share of the code words the
+// packing ORs into (round_up(codes_len, 4) bytes, sized on the device), sums the
+// code lengths of kScanTile blocks (HuffmanUtil.cpp:1103-1128 counts bits per block
+// the same way), scans them in place and records the tile total; the last
+// workgroup to finish (a ticket in meta[kTicket], reset by enc_tree_kernel) turns
+// the tile totals into tile offsets.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan over the kScanTile threads of a workgroup: wave scans, then one
+// wave scans the 16 wave totals (s_w: 16 words of LDS). Returns the prefix; *total
+// gets the workgroup's sum. Ends with a barrier, so s_w may be reused at once.
+__device__ __forceinline__ uint32_t wg_exclusive_scan(uint32_t x, uint32_t *s_w, uint32_t *total) {
+  constexpr uint32_t kWaves = kScanTile / 64;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_inclusive_scan(x);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t v = wave_inclusive_scan(lane < kWaves ? s_w[lane] : 0u);
+    if (lane < kWaves) s_w[lane] = v;
+  }
+  __syncthreads();
+  const uint32_t base = wave ? s_w[wave - 1] : 0u;
+  *total = s_w[kWaves - 1];
+  __syncthreads();
+  return base + incl - x;
+}
+
+__global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym, const uint32_t *table,
+                                                             uint64_t nb, uint32_t *bpre, uint32_t *tsum,
+                                                             uint64_t *meta, uint32_t *words) {
   __shared__ uint32_t len[256];
-  len[threadIdx.x] = table[threadIdx.x] & 0xFFu;
+  __shared__ uint32_t s_w[kScanTile / 64];
+  __shared__ uint32_t last;
+  const uint32_t tid = threadIdx.x;
+  if (tid < 256) len[tid] = table[tid] & 0xFFu;
+  const uint64_t nw = meta[1] ? (meta[0] + 3) / 4 : 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kScanTile + tid; i < nw; i += (uint64_t)gridDim.x * kScanTile)
+    words[i] = 0;
   __syncthreads();
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
-  const uint64_t *src = reinterpret_cast<const uint64_t *>(sym + b * 64);
-  uint32_t n = 0;
-  for (int k = 0; k < 8; ++k) {
-    const uint64_t q = src[k];
-    for (int j = 0; j < 8; ++j) n += len[(q >> (8 * j)) & 0xFF];
-  }
-  blen[b] = n;
-}
-
-// Exclusive scan, level 1: each workgroup scans kScanTile block lengths in place
-// and records the tile total.
-__global__ void __launch_bounds__(kScanTile) enc_scan_tiles(uint32_t *blen, uint64_t nb, uint32_t *tsum) {
-  __shared__ uint32_t s[kScanTile];
-  const uint64_t i = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
-  const uint32_t x = i < nb ? blen[i] : 0u;
-  s[threadIdx.x] = x;
-  __syncthreads();
-  for (uint32_t d = 1; d < kScanTile; d <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0u;
-    __syncthreads();
-    s[threadIdx.x] += add;
-    __syncthreads();
-  }
-  if (i < nb) blen[i] = s[threadIdx.x] - x;
-  if (threadIdx.x == kScanTile - 1) tsum[blockIdx.x] = s[threadIdx.x];
-}
-
-// Level 2: one workgroup turns the tile totals into tile offsets (serial chunks).
-__global__ void __launch_bounds__(kScanTile) enc_scan_totals(uint32_t *tsum, uint64_t ntiles) {
-  __shared__ uint32_t s[kScanTile];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint64_t base = 0; base < ntiles; base += kScanTile) {
-    const uint64_t i = base + threadIdx.x;
-    const uint32_t x = i < ntiles ? tsum[i] : 0u;
-    s[threadIdx.x] = x;
-    __syncthreads();
-    for (uint32_t d = 1; d < kScanTile; d <<= 1) {
-      const uint32_t add = threadIdx.x >= d ? s[threadIdx.x - d] : 0u;
-      __syncthreads();
-      s[threadIdx.x] += add;
-      __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * kScanTile + tid;
+  uint32_t x = 0;
+  if (i < nb) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(sym + i * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t q = src[k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x += len[(q >> (8 * j)) & 0xFF];
     }
-    if (i < ntiles) tsum[i] = carry + s[threadIdx.x] - x;
-    __syncthreads();
-    if (threadIdx.x == kScanTile - 1) carry += s[threadIdx.x];
-    __syncthreads();
+  }
+  uint32_t total;
+  const uint32_t pre = wg_exclusive_scan(x, s_w, &total);
+  if (i < nb) bpre[i] = pre;
+  if (tid == 0) {
+    tsum[blockIdx.x] = total;
+    __threadfence();
+    last = atomicAdd(reinterpret_cast<uint32_t *>(&meta[kTicket]), 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const uint64_t ntiles = gridDim.x;
+  uint32_t carry = 0;
+  for (uint64_t base = 0; base < ntiles; base += kScanTile) {
+    const uint64_t t = base + tid;
+    // other workgroups' totals: device-coherent loads (past this CU's L1)
+    const uint32_t v = t < ntiles ? __hip_atomic_load(&tsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t chunk;
+    const uint32_t p = wg_exclusive_scan(v, s_w, &chunk);
+    if (t < ntiles) tsum[t] = carry + p;
+    carry += chunk;
   }
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
 
-// Level 3 + packing: block b's offset = its in-tile prefix + its tile's offset;
-// the block's 64 codes go out MSB-first as big-endian words. Interior words are
-// the block's alone (plain stores); its first and last word may be shared with
-// the neighbouring blocks (atomic OR into the zeroed buffer).
-__global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const uint32_t *table,
-                                                       const uint32_t *blen_prefix, const uint32_t *toff,
-                                                       uint64_t nb, uint32_t *offsets, uint32_t *words) {
+// Level 3 + packing, staged in LDS: a workgroup's 256 blocks own one contiguous
+// bit range (at most 256 x 64 x 16 bits). Each thread packs its block's codes
+// MSB-first into big-endian words of that range in LDS (OR-ing only the two words
+// it may share with its neighbours), then the workgroup writes the range out in
+// order: interior words with plain coalesced stores, its first and last word
+// (shared with the neighbouring workgroups) with an atomic OR into the zeroed buffer.
+constexpr uint32_t kPackBlocks = 256;
+constexpr uint32_t kPackWords = kPackBlocks * 64 * 16 / 32 + 2;
+__global__ void __launch_bounds__(kPackBlocks) enc_pack_kernel(const uint8_t *sym, const uint32_t *table,
+                                                               const uint32_t *blen_prefix, const uint32_t *toff,
+                                                               uint64_t nb, uint32_t *offsets, uint32_t *words,
+                                                               const uint64_t *meta) {
   __shared__ uint32_t tab[256];
-  tab[threadIdx.x] = table[threadIdx.x];
+  __shared__ uint32_t lw[kPackWords];
+  __shared__ uint32_t s_start, s_end;  // bit range of this workgroup's blocks
+  const uint32_t tid = threadIdx.x;
+  if (!meta[1]) return;  // a rejected frame (status) writes nothing
+  tab[tid] = table[tid];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlocks, b = b0 + tid;
+  const bool on = b < nb;
+  const uint32_t o = on ? blen_prefix[b] + toff[b / kScanTile] : 0u;
+  if (on) offsets[b] = o;
+  if (tid == 0) {
+    const uint64_t bn = b0 + kPackBlocks;
+    s_start = o;
+    s_end = bn < nb ? blen_prefix[bn] + toff[bn / kScanTile] : (uint32_t)meta[kTotalBits];
+  }
   __syncthreads();
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
-  const uint32_t o = blen_prefix[b] + toff[b / kScanTile];
-  offsets[b] = o;
-  const uint64_t *src = reinterpret_cast<const uint64_t *>(sym + b * 64);
-  uint32_t widx = o >> 5, used = o & 31u, cur = 0;
-  bool first = true;
-  auto emit = [&](bool shared) {
-    if (shared) atomicOr(&words[widx], bswap32(cur));
-    else words[widx] = bswap32(cur);
-  };
-  for (int k = 0; k < 8; ++k) {
-    const uint64_t q = src[k];
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t e = tab[(q >> (8 * j)) & 0xFF];
-      const uint32_t len = e & 0xFFu;
-      const uint32_t c = (e >> 16) >> (16 - len);  // right-aligned code
-      if (used + len < 32) {
-        cur |= c << (32 - used - len);
-        used += len;
-      } else {  // the word fills up
-        const uint32_t spill = used + len - 32;
-        cur |= c >> spill;
-        emit(first);
-        first = false;
-        ++widx;
-        cur = spill ? c << (32 - spill) : 0u;
-        used = spill;
+  const uint32_t w0 = s_start >> 5, nwords = ((s_end + 31) >> 5) - w0;
+  for (uint32_t i = tid; i < nwords; i += kPackBlocks) lw[i] = 0;
+  __syncthreads();
+  if (on) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(sym + b * 64);
+    uint32_t widx = (o >> 5) - w0, used = o & 31u, cur = 0;
+    bool first = true;
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t q = src[k];
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t e = tab[(q >> (8 * j)) & 0xFF];
+        const uint32_t len = e & 0xFFu;
+        const uint32_t c = (e >> 16) >> (16 - len);  // right-aligned code
+        if (used + len < 32) {
+          cur |= c << (32 - used - len);
+          used += len;
+        } else {  // the word fills up
+          const uint32_t spill = used + len - 32;
+          cur |= c >> spill;
+          if (first) atomicOr(&lw[widx], bswap32(cur));
+          else lw[widx] = bswap32(cur);
+          first = false;
+          ++widx;
+          cur = spill ? c << (32 - spill) : 0u;
+          used = spill;
+        }
       }
     }
+    if (used) atomicOr(&lw[widx], bswap32(cur));  // last, partial word: the next block may share it
   }
-  if (used) emit(true);  // last, partial word: the next block may share it
+  __syncthreads();
+  for (uint32_t i = tid; i < nwords; i += kPackBlocks) {
+    const uint32_t v = lw[i];
+    if (i == 0 || i == nwords - 1) {
+      if (v) atomicOr(&words[w0 + i], v);
+    } else {
+      words[w0 + i] = v;
+    }
+  }
 }
 
 }  // namespace
 
 extern "C" {
 
-size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height) {
+// mh_encode_frame_device_async's workspace; mh_encode_frame_device needs kResultBytes
+// more (see mh_encode_workspace_bytes in the header: it reports the larger figure).
+static size_t async_workspace_bytes(uint32_t width, uint32_t height) {
   const uint64_t nb = (uint64_t)((width + 7) / 8) * ((height + 7) / 8);
   return (size_t)carve(nullptr, nb, nullptr);
 }
 
-int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
-                           uint8_t canon_header[256], uint8_t *d_codes, uint64_t codes_cap,
-                           uint64_t *codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
-                           void *d_workspace, size_t workspace_bytes, void *stream) {
-  if (!d_gray || !canon_header || !d_codes || !codes_len || !d_block_offsets || !d_workspace)
+size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height) {
+  return async_workspace_bytes(width, height) + kResultBytes;
+}
+
+int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
+                                 uint8_t *d_canon_header, uint8_t *d_codes, uint64_t codes_cap,
+                                 uint64_t *d_codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                                 int32_t *d_status, void *d_workspace, size_t workspace_bytes, void *stream) {
+  if (!d_gray || !d_canon_header || !d_codes || !d_block_offsets || !d_workspace)
     return MH_ERR_INVALID_ARG;
   if (flags & ~MH_FLAG_NO_DELTA) return MH_ERR_INVALID_ARG;
   if (!width || !height || width > MH_MAX_DIM || height > MH_MAX_DIM) return MH_ERR_DIMS;
   if (((uintptr_t)d_codes & 3u) || ((uintptr_t)d_workspace & 255u)) return MH_ERR_ALIGN;
   const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
   const uint64_t nb = (uint64_t)bw * bh;
-  if (workspace_bytes < mh_encode_workspace_bytes(width, height)) return MH_ERR_CAPACITY;
+  if (workspace_bytes < async_workspace_bytes(width, height)) return MH_ERR_CAPACITY;
   Workspace w;
   carve(static_cast<uint8_t *>(d_workspace), nb, &w);
   hipStream_t s = (hipStream_t)stream;
@@ -233,42 +494,43 @@ int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t heigh
   if (g256 == 0 || ntiles > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
 
   if (hipMemsetAsync(w.hist, 0, 256 * 8, s) != hipSuccess) return MH_ERR_HIP;
-  hipLaunchKernelGGL(enc_split_kernel, dim3(g256), dim3(256), 0, s, d_gray, width, height, bw, nb, flags,
+  const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
+  const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, MH_SPLIT_WGS);
+  hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
                      w.sym, d_block_init, w.hist);
-  uint64_t hist[256];
-  if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(hist, w.hist, sizeof(hist), hipMemcpyDeviceToHost, s) != hipSuccess ||
+  hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(256), 0, s, w.hist, d_canon_header, w.table, w.meta,
+                     d_codes_len, codes_cap, d_status);
+  hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
+                     w.tsum, w.meta, reinterpret_cast<uint32_t *>(d_codes));
+  hipLaunchKernelGGL(enc_pack_kernel, dim3(g256), dim3(256), 0, s, w.sym, w.table, w.blen, w.tsum, nb,
+                     d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), w.meta);
+  return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
+}
+
+int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
+                           uint8_t canon_header[256], uint8_t *d_codes, uint64_t codes_cap,
+                           uint64_t *codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                           void *d_workspace, size_t workspace_bytes, void *stream) {
+  if (!canon_header || !codes_len) return MH_ERR_INVALID_ARG;
+  if (workspace_bytes < mh_encode_workspace_bytes(width, height)) return MH_ERR_CAPACITY;
+  // header, byte count and status land at the end of the workspace, then come over
+  // in one copy and one synchronisation
+  uint8_t *res = static_cast<uint8_t *>(d_workspace) + (workspace_bytes - kResultBytes) / 256 * 256;
+  int rc = mh_encode_frame_device_async(d_gray, width, height, flags, res, d_codes, codes_cap,
+                                        reinterpret_cast<uint64_t *>(res + 256), d_block_offsets, d_block_init,
+                                        reinterpret_cast<int32_t *>(res + 264), d_workspace,
+                                        (workspace_bytes - kResultBytes) / 256 * 256, stream);
+  if (rc != MH_OK) return rc;
+  uint8_t host[kResultBytes];
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(host, res, kResultBytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MH_ERR_HIP;
-
-  // host: the reference's tree on 256 counts, canonical codes, sizes
-  int rc = mh_code_lengths(hist, canon_header);
-  if (rc != MH_OK) return rc;
-  uint16_t cc[256];
-  rc = mh_canonical_codes(canon_header, cc);
-  if (rc != MH_OK) return rc;
-  uint64_t total_bits = 0;
-  uint32_t table[256];
-  for (int i = 0; i < 256; ++i) {
-    total_bits += hist[i] * canon_header[i];
-    table[i] = ((uint32_t)cc[i] << 16) | canon_header[i];
-  }
-  if (total_bits >= (1ull << 32)) return MH_ERR_CAPACITY;  // u32 block offsets
-  const uint64_t payload = (total_bits + 7) / 8;
-  const uint64_t len = payload + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
-  const uint64_t zero_bytes = (len + 3) & ~3ull;
-  if (zero_bytes > codes_cap) return MH_ERR_CAPACITY;
-
-  if (hipMemcpyAsync(w.table, table, sizeof(table), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemsetAsync(d_codes, 0, zero_bytes, s) != hipSuccess)
-    return MH_ERR_HIP;
-  hipLaunchKernelGGL(enc_blen_kernel, dim3(g256), dim3(256), 0, s, w.sym, w.table, nb, w.blen);
-  hipLaunchKernelGGL(enc_scan_tiles, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.blen, nb, w.tsum);
-  hipLaunchKernelGGL(enc_scan_totals, dim3(1), dim3(kScanTile), 0, s, w.tsum, ntiles);
-  hipLaunchKernelGGL(enc_pack_kernel, dim3(g256), dim3(256), 0, s, w.sym, w.table, w.blen, w.tsum, nb,
-                     d_block_offsets, reinterpret_cast<uint32_t *>(d_codes));
-  if (hipGetLastError() != hipSuccess) return MH_ERR_HIP;
-  *codes_len = len;
+  int32_t status;
+  std::memcpy(&status, host + 264, 4);
+  if (status != MH_OK) return status;
+  std::memcpy(canon_header, host, 256);
+  std::memcpy(codes_len, host + 256, 8);
   return MH_OK;
 }
 

@@ -2,6 +2,9 @@
 
 Byte-identical to the host codec (codec.encode_frame), so frames encoded on the GPU
 feed the decoder -- and the reference's own renderer contract -- unchanged.
+Encoder.encode returns the header and byte count on the host (one synchronisation);
+Encoder.encode_async (mh_encode_frame_device_async) leaves everything on the device,
+so an encode -> table build -> decode chain never waits on the host.
 """
 from __future__ import annotations
 
@@ -68,6 +71,68 @@ class Encoder:
             aligned, self.workspace.numel() - (aligned - base), _stream_ptr(stream, self.device)),
             "mh_encode_frame_device")
         return DeviceEncodedFrame(self.width, self.height, canon, codes[: n.value], offs, init, flags)
+
+    def encode_async(self, gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False,
+                     stream: Optional[torch.cuda.Stream] = None,
+                     codes: Optional[torch.Tensor] = None) -> AsyncEncodedFrame:
+        """Enqueue the encode on `stream` (default: the current stream) and return
+        at once. `codes` may be a reused u8 buffer of at least the encoder's
+        capacity (the default allocates one)."""
+        if gray.dtype != torch.uint8 or gray.shape != (self.height, self.width) or not gray.is_contiguous():
+            raise ValueError(f"gray must be contiguous uint8 [{self.height}, {self.width}]")
+        if gray.device != self.device:
+            raise ValueError("gray must live on the encoder's device")
+        if codes is None:
+            codes = torch.empty(self.cap, dtype=torch.uint8, device=self.device)
+        if codes.dtype != torch.uint8 or codes.device != self.device or codes.numel() < 4:
+            raise ValueError("codes must be a uint8 buffer on the encoder's device")
+        offs = torch.empty(self.nb, dtype=torch.int32, device=self.device)
+        init = torch.empty(self.nb, dtype=torch.uint8, device=self.device) if init_zero_delta else None
+        canon = torch.empty(256, dtype=torch.uint8, device=self.device)
+        meta = torch.empty(2, dtype=torch.int64, device=self.device)   # [codes_len, status]
+        base = self.workspace.data_ptr()
+        aligned = (base + 255) // 256 * 256
+        N.check(N.lib().mh_encode_frame_device_async(
+            gray.data_ptr(), self.width, self.height, flags, canon.data_ptr(), codes.data_ptr(),
+            codes.numel(), meta.data_ptr(), offs.data_ptr(), init.data_ptr() if init is not None else None,
+            meta.data_ptr() + 8, aligned, self.workspace.numel() - (aligned - base),
+            _stream_ptr(stream, self.device)), "mh_encode_frame_device_async")
+        return AsyncEncodedFrame(self.width, self.height, canon, codes, meta[0:1],
+                                 meta[1:2].view(torch.int32)[0:1], offs, init, flags)
+
+
+@dataclasses.dataclass
+class AsyncEncodedFrame:
+    """An encode still in flight on the device: header, byte count and status are
+    device tensors. frames()/tables() chain the decode without a host sync;
+    result() synchronises and returns the DeviceEncodedFrame (raising MHError on
+    a rejected frame)."""
+    width: int
+    height: int
+    canon: torch.Tensor               # u8[256] on the device
+    codes: torch.Tensor               # u8[capacity] on the device (first codes_len bytes used)
+    codes_len: torch.Tensor           # int64[1] on the device (0 on an error)
+    status: torch.Tensor              # int32[1] on the device
+    block_offsets: torch.Tensor
+    block_init: Optional[torch.Tensor]
+    flags: int
+
+    def frames(self) -> DeviceFrames:
+        """A one-frame DeviceFrames over the whole code buffer (the decoder bounds
+        the last block by its offset, not by the buffer size)."""
+        return DeviceFrames(self.width, self.height, 1, self.block_offsets, self.codes, None,
+                            self.block_init, self.flags, int(self.codes.numel()) - N.MH_CODES_PAD)
+
+    def tables(self, prepare_lut: bool = True, stream: Optional[torch.cuda.Stream] = None):
+        """T1/T2 (+ prepared table) built on the device from the device header."""
+        from .decoder import DeviceTables
+        return DeviceTables.from_canonical_header(self.canon, self.canon.device, prepare_lut, stream)
+
+    def result(self) -> DeviceEncodedFrame:
+        st, n = int(self.status.item()), int(self.codes_len.item())
+        N.check(st, "mh_encode_frame_device_async")
+        return DeviceEncodedFrame(self.width, self.height, self.canon.cpu().numpy(), self.codes[:n],
+                                  self.block_offsets, self.block_init, self.flags)
 
 
 def encode_frame_device(gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False) -> DeviceEncodedFrame:

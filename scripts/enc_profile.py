@@ -1,0 +1,41 @@
+"""Run the device-only encoder on BigBridge-shuffled frames (for rocprofv3
+--kernel-trace --stats: per-kernel times of split / tree / zero / blen / scan / pack)."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from metalhuffman_amd import frames as F  # noqa: E402
+from metalhuffman_amd.encoder import Encoder  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+bb = F.bigbridge()
+dev = torch.device("cuda:0")
+imgs = [torch.from_numpy(F.block_shuffle(bb, 900 + k)).to(dev) for k in range(4)]
+enc = Encoder(bb.shape[1], bb.shape[0], dev)
+codes = [torch.empty(enc.cap, dtype=torch.uint8, device=dev) for _ in range(4)]
+for k in range(8):
+    enc.encode_async(imgs[k % 4], codes=codes[k % 4])
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for k in range(reps):
+    enc.encode_async(imgs[k % 4], codes=codes[k % 4])
+torch.cuda.synchronize()
+print(f"async encode {1e6 * (time.perf_counter() - t0) / reps:.1f} us/frame")
+
+if len(sys.argv) > 2 and sys.argv[2] == "stamps":
+    # library built with -DMH_TREE_STAMPS=1: s_memtime at the tree kernel's phase
+    # boundaries in meta[2..10] (meta = the last 256 bytes of the async workspace)
+    from metalhuffman_amd import _native as N
+    ws = int(N.lib().mh_encode_workspace_bytes(bb.shape[1], bb.shape[0]))
+    base = enc.workspace.data_ptr()
+    off = (base + 255) // 256 * 256 - base + (ws - 512) - 256
+    for k in range(3):
+        enc.encode_async(imgs[k], codes=codes[k])
+        torch.cuda.synchronize()
+        m = enc.workspace[off: off + 88].cpu().view(torch.int64).tolist()
+        st = m[2:11]
+        print("tree phases (s_memtime clocks): load", st[1] - st[0], "rank", st[2] - st[1], "merge", st[3] - st[2],
+              "jump-init", st[4] - st[3], "jump+lengths", st[5] - st[4], "ballots", st[6] - st[5],
+              "first-codes", st[7] - st[6], "table", st[8] - st[7], "total", st[8] - st[0])

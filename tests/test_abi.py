@@ -110,6 +110,17 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_encode_frame_device(0x100, 8, 8, 0, canon, 0x1000, 64, ctypes.byref(n), 0x2000, None,
                                     0x10000, 16, None) == -4
     assert L.mh_encode_workspace_bytes(2048, 1536) >= 49152 * 64
+    ws = L.mh_encode_workspace_bytes(64, 64)
+    assert L.mh_encode_frame_device_async(None, 8, 8, 0, 0x3000, 0x1000, 64, None, 0x2000, None, None,
+                                          0x10000, ws, None) == -1
+    assert L.mh_encode_frame_device_async(0x100, 8, 8, 2, 0x3000, 0x1000, 64, None, 0x2000, None, None,
+                                          0x10000, ws, None) == -1
+    assert L.mh_encode_frame_device_async(0x100, 8, 70000, 0, 0x3000, 0x1000, 64, None, 0x2000, None,
+                                          None, 0x10000, ws, None) == -2
+    assert L.mh_encode_frame_device_async(0x100, 8, 8, 0, 0x3000, 0x1000, 64, None, 0x2000, None, None,
+                                          0x10080, ws, None) == -6
+    assert L.mh_encode_frame_device_async(0x100, 64, 64, 0, 0x3000, 0x1000, 64, None, 0x2000, None,
+                                          None, 0x10000, 256, None) == -4
     assert L.mh_check(None, 0x70000, None) == -1
     assert L.mh_check(ctypes.byref(_frame()), None, None) == -1
     assert L.mh_check(ctypes.byref(_frame(n_frames=2)), 0x70000, None) == -1

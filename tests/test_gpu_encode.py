@@ -62,3 +62,94 @@ def test_encode_too_long_code_is_rejected(mh, device):
     with pytest.raises(mh.MHError) as ei:
         encode_frame_device(torch.from_numpy(img).to(device))
     assert ei.value.status == -3
+
+
+# ---- mh_encode_frame_device_async: the tree on the device, no host sync ----
+
+def _check_async(mh, device, img, flags=0, init_zero=False):
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd.encoder import Encoder
+    host = mh.encode_frame(img, flags=flags, init_zero_delta=init_zero)
+    h, w = img.shape
+    enc = Encoder(w, h, device)
+    a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).to(device), flags, init_zero)
+    # decode straight from the device header and the whole code buffer, then look
+    out = D.decode(a.frames(), a.tables())
+    torch.cuda.synchronize(device)
+    assert int(a.status.item()) == 0
+    assert int(a.codes_len.item()) == host.codes.size
+    assert np.array_equal(a.canon.cpu().numpy(), host.canon)
+    assert np.array_equal(a.codes[: host.codes.size].cpu().numpy(), host.codes)
+    assert np.array_equal(a.block_offsets.cpu().numpy().view(np.uint32), host.block_offsets)
+    if init_zero:
+        assert np.array_equal(a.block_init.cpu().numpy(), host.block_init)
+    assert np.array_equal(out[0, :, :w].cpu().numpy(), img)
+    r = a.result()
+    assert r.codes.numel() == host.codes.size and np.array_equal(r.canon, host.canon)
+
+
+def test_async_encode_bigbridge_and_variants(mh, device, bigbridge):
+    from metalhuffman_amd import frames as F
+    _check_async(mh, device, bigbridge)
+    _check_async(mh, device, np.ascontiguousarray(bigbridge[:777, :1001]), init_zero=True)
+    _check_async(mh, device, F.uniform_random(256, 320, 77))
+    _check_async(mh, device, fibonacci_deltas(17, 128 * 128, seed=8).reshape(128, 128), flags=1)
+    _check_async(mh, device, np.full((9, 17), 200, np.uint8))          # one delta symbol (0)
+    _check_async(mh, device, np.full((16, 16), 7, np.uint8), flags=1)   # one raw symbol
+
+
+def _deltas_with_histogram(counts: np.ndarray, seed: int) -> np.ndarray:
+    d = np.repeat(np.arange(256, dtype=np.uint8), counts.astype(np.int64))
+    np.random.default_rng(seed).shuffle(d)
+    return d
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_async_tree_matches_reference_tie_breaking(mh, device, seed):
+    """Histograms full of equal weights (where the reference's upper_bound insertion
+    decides the tree), random small counts and a Fibonacci-like ladder up to depth
+    16: the device tree must give the host codec's header (mh_code_lengths, pinned
+    to the reference encoder) byte for byte."""
+    rng = np.random.default_rng(100 + seed)
+    k = int(rng.integers(2, 257))
+    syms = rng.choice(256, k, replace=False)
+    counts = np.zeros(256, np.int64)
+    kind = seed % 3
+    if kind == 0:
+        counts[syms] = 64                               # all equal
+    elif kind == 1:
+        counts[syms] = rng.integers(1, 6, k) * 8        # many ties
+    else:
+        fib = [1, 1]
+        while len(fib) < min(k, 16):
+            fib.append(fib[-1] + fib[-2])
+        counts[syms[: len(fib)]] = np.array(fib) * 8
+        counts[syms[len(fib):]] = 8
+    total = int(counts.sum())
+    side = 8 * int(np.ceil(np.sqrt(total / 64.0)))
+    counts[syms[0]] += side * side - total             # pad to a whole square of blocks
+    d = _deltas_with_histogram(counts, seed)
+    img = image_from_block_deltas(d, side, side)
+    _check_async(mh, device, img)
+
+
+def test_async_encode_errors_write_nothing(mh, device):
+    import torch
+    from metalhuffman_amd.encoder import Encoder
+    img = image_from_block_deltas(fibonacci_deltas(18, 256 * 256, seed=1), 256, 256)
+    enc = Encoder(256, 256, device)
+    codes = torch.full((enc.cap,), 0xAB, dtype=torch.uint8, device=device)
+    a = enc.encode_async(torch.from_numpy(img).to(device), codes=codes)
+    torch.cuda.synchronize(device)
+    assert int(a.status.item()) == -3 and int(a.codes_len.item()) == 0
+    assert bool((codes == 0xAB).all())
+    with pytest.raises(mh.MHError):
+        a.result()
+    # a code buffer too small for the frame: MH_ERR_CAPACITY on the device
+    from metalhuffman_amd import frames as F
+    small = torch.full((1024,), 0xCD, dtype=torch.uint8, device=device)
+    b = enc.encode_async(torch.from_numpy(F.uniform_random(256, 256, 5)).to(device), codes=small)
+    torch.cuda.synchronize(device)
+    assert int(b.status.item()) == -4 and int(b.codes_len.item()) == 0
+    assert bool((small == 0xCD).all())
