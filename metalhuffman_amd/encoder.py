@@ -8,6 +8,7 @@ so an encode -> table build -> decode chain never waits on the host.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import dataclasses
 from typing import Optional
@@ -41,7 +42,9 @@ class DeviceEncodedFrame:
 
 
 class Encoder:
-    """Reusable device workspace + output buffers for frames of one size."""
+    """Reusable device workspace + output buffers for frames of one size. Calls on
+    one stream queue up behind each other; frames in flight on several streams need
+    one Encoder (one workspace) per stream."""
 
     def __init__(self, width: int, height: int, device="cuda"):
         self.device = _dev(device)
@@ -82,14 +85,17 @@ class Encoder:
             raise ValueError(f"gray must be contiguous uint8 [{self.height}, {self.width}]")
         if gray.device != self.device:
             raise ValueError("gray must live on the encoder's device")
-        if codes is None:
-            codes = torch.empty(self.cap, dtype=torch.uint8, device=self.device)
+        # outputs belong to the stream the kernels run on (the caching allocator must
+        # not hand their memory out again while that stream still writes it)
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            if codes is None:
+                codes = torch.empty(self.cap, dtype=torch.uint8, device=self.device)
+            offs = torch.empty(self.nb, dtype=torch.int32, device=self.device)
+            init = torch.empty(self.nb, dtype=torch.uint8, device=self.device) if init_zero_delta else None
+            canon = torch.empty(256, dtype=torch.uint8, device=self.device)
+            meta = torch.empty(2, dtype=torch.int64, device=self.device)   # [codes_len, status]
         if codes.dtype != torch.uint8 or codes.device != self.device or codes.numel() < 4:
             raise ValueError("codes must be a uint8 buffer on the encoder's device")
-        offs = torch.empty(self.nb, dtype=torch.int32, device=self.device)
-        init = torch.empty(self.nb, dtype=torch.uint8, device=self.device) if init_zero_delta else None
-        canon = torch.empty(256, dtype=torch.uint8, device=self.device)
-        meta = torch.empty(2, dtype=torch.int64, device=self.device)   # [codes_len, status]
         base = self.workspace.data_ptr()
         aligned = (base + 255) // 256 * 256
         N.check(N.lib().mh_encode_frame_device_async(
