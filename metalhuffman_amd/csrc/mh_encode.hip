@@ -27,7 +27,7 @@
 
 namespace {
 
-constexpr uint32_t kScanTile = 1024;  // blocks per workgroup in the offsets scan
+constexpr uint32_t kScanTile = 256;  // blocks per workgroup in the offsets scan
 constexpr uint32_t kResultBytes = 512;  // mh_encode_frame_device: header, byte count, status
 constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
@@ -86,21 +86,25 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint32_t r = threadIdx.x & 7u;
   const uint32_t copy = threadIdx.x % kHistCopies;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
+  // one block row (8 pixels) of group g, zero past the frame edge
+  auto load_row = [&](uint64_t g) -> uint64_t {
+    const uint64_t b = g * 32 + (threadIdx.x >> 3);
+    if (b >= nb) return 0;
+    const uint32_t bx = (uint32_t)(b % bw), y = (uint32_t)(b / bw) * 8 + r;
+    if (y >= H) return 0;
+    const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
+    if (vec) return *reinterpret_cast<const uint64_t *>(row);  // W % 8 == 0, 8-byte aligned frame
+    uint64_t q = 0;
+    for (uint32_t c = 0; c < 8; ++c)
+      if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
+    return q;
+  };
+  uint64_t q_next = load_row(blockIdx.x);
   for (uint64_t g = blockIdx.x; g * 32 < nb; g += gridDim.x) {
     const uint64_t b = g * 32 + (threadIdx.x >> 3);
     const bool on = b < nb;
-    const uint32_t bx = on ? (uint32_t)(b % bw) : 0u, by = on ? (uint32_t)(b / bw) : 0u;
-    const uint32_t y = by * 8 + r;
-    uint64_t q = 0;
-    if (on && y < H) {
-      const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
-      if (vec) {  // W % 8 == 0 and an 8-byte aligned frame: every block row is inside
-        q = *reinterpret_cast<const uint64_t *>(row);
-      } else {
-        for (uint32_t c = 0; c < 8; ++c)
-          if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
-      }
-    }
+    const uint64_t q = q_next;
+    q_next = load_row(g + gridDim.x);  // next group's row in flight while this one is processed
     uint64_t v = q;
     if (delta) {
       // previous pixel: the last pixel of the row above in the same block, 0 for row 0
@@ -368,13 +372,19 @@ __global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym,
   const uint32_t pre = wg_exclusive_scan(x, s_w, &total);
   if (i < nb) bpre[i] = pre;
   if (tid == 0) {
-    tsum[blockIdx.x] = total;
-    __threadfence();
-    last = atomicAdd(reinterpret_cast<uint32_t *>(&meta[kTicket]), 1u) == gridDim.x - 1 ? 1u : 0u;
+    // The tile total goes out as a device-scope store (written through past this
+    // XCD's L2) and is acknowledged before the ticket is taken, so the last
+    // workgroup's device-scope loads see every total. A __threadfence() here would
+    // write back this XCD's whole L2 (buffer_wbl2) in every workgroup: 1 us more.
+    __hip_atomic_store(&tsum[blockIdx.x], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kTicket]), 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1
+               ? 1u
+               : 0u;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   const uint64_t ntiles = gridDim.x;
   uint32_t carry = 0;
   for (uint64_t base = 0; base < ntiles; base += kScanTile) {
@@ -390,66 +400,79 @@ __global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym,
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
 
-// Level 3 + packing, staged in LDS: a workgroup's 256 blocks own one contiguous
-// bit range (at most 256 x 64 x 16 bits). Each thread packs its block's codes
-// MSB-first into big-endian words of that range in LDS (OR-ing only the two words
-// it may share with its neighbours), then the workgroup writes the range out in
-// order: interior words with plain coalesced stores, its first and last word
-// (shared with the neighbouring workgroups) with an atomic OR into the zeroed buffer.
-constexpr uint32_t kPackBlocks = 256;
+// Level 3 + packing, staged in LDS. Eight lanes per block, eight symbols each: a
+// lane's bit position is its block's offset plus the code lengths of the lanes
+// before it (a shuffle scan in the 8-lane group), so the serial chain is 8 symbols,
+// not 64. A workgroup's 32 blocks own one contiguous bit range; lanes pack their
+// bits MSB-first into big-endian words of that range in LDS (OR-ing the first and
+// last word, which neighbouring lanes may share), then the workgroup writes the
+// range out with coalesced stores, OR-ing only its first and last word (shared with
+// the neighbouring workgroups) into the zeroed buffer.
+constexpr uint32_t kPackBlocks = 32;
 constexpr uint32_t kPackWords = kPackBlocks * 64 * 16 / 32 + 2;
-__global__ void __launch_bounds__(kPackBlocks) enc_pack_kernel(const uint8_t *sym, const uint32_t *table,
-                                                               const uint32_t *blen_prefix, const uint32_t *toff,
-                                                               uint64_t nb, uint32_t *offsets, uint32_t *words,
-                                                               const uint64_t *meta) {
+__global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const uint32_t *table,
+                                                       const uint32_t *blen_prefix, const uint32_t *toff,
+                                                       uint64_t nb, uint32_t *offsets, uint32_t *words,
+                                                       const uint64_t *meta) {
   __shared__ uint32_t tab[256];
   __shared__ uint32_t lw[kPackWords];
   __shared__ uint32_t s_start, s_end;  // bit range of this workgroup's blocks
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, part = tid & 7u;
   if (!meta[1]) return;  // a rejected frame (status) writes nothing
   tab[tid] = table[tid];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlocks, b = b0 + tid;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlocks, b = b0 + (tid >> 3);
   const bool on = b < nb;
   const uint32_t o = on ? blen_prefix[b] + toff[b / kScanTile] : 0u;
-  if (on) offsets[b] = o;
+  if (on && part == 0) offsets[b] = o;
   if (tid == 0) {
     const uint64_t bn = b0 + kPackBlocks;
     s_start = o;
     s_end = bn < nb ? blen_prefix[bn] + toff[bn / kScanTile] : (uint32_t)meta[kTotalBits];
   }
+  const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
   __syncthreads();
   const uint32_t w0 = s_start >> 5, nwords = ((s_end + 31) >> 5) - w0;
-  for (uint32_t i = tid; i < nwords; i += kPackBlocks) lw[i] = 0;
+  for (uint32_t i = tid; i < nwords; i += 256) lw[i] = 0;
+  uint32_t e[8], nbits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    e[j] = tab[(q >> (8 * j)) & 0xFF];
+    nbits += e[j] & 0xFFu;
+  }
+  uint32_t pre = nbits;  // inclusive scan over the block's 8 lanes
+#pragma unroll
+  for (uint32_t d = 1; d < 8; d <<= 1) {
+    const uint32_t y = __shfl_up(pre, d, 8);
+    if (part >= d) pre += y;
+  }
+  pre -= nbits;
   __syncthreads();
   if (on) {
-    const uint64_t *src = reinterpret_cast<const uint64_t *>(sym + b * 64);
-    uint32_t widx = (o >> 5) - w0, used = o & 31u, cur = 0;
+    const uint32_t start = o + pre - (w0 << 5);
+    uint32_t widx = start >> 5, used = start & 31u, cur = 0;
     bool first = true;
-    for (int k = 0; k < 8; ++k) {
-      const uint64_t q = src[k];
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t e = tab[(q >> (8 * j)) & 0xFF];
-        const uint32_t len = e & 0xFFu;
-        const uint32_t c = (e >> 16) >> (16 - len);  // right-aligned code
-        if (used + len < 32) {
-          cur |= c << (32 - used - len);
-          used += len;
-        } else {  // the word fills up
-          const uint32_t spill = used + len - 32;
-          cur |= c >> spill;
-          if (first) atomicOr(&lw[widx], bswap32(cur));
-          else lw[widx] = bswap32(cur);
-          first = false;
-          ++widx;
-          cur = spill ? c << (32 - spill) : 0u;
-          used = spill;
-        }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t len = e[j] & 0xFFu;
+      const uint32_t c = (e[j] >> 16) >> (16 - len);  // right-aligned code
+      if (used + len < 32) {
+        cur |= c << (32 - used - len);
+        used += len;
+      } else {  // the word fills up
+        const uint32_t spill = used + len - 32;
+        cur |= c >> spill;
+        if (first) atomicOr(&lw[widx], bswap32(cur));
+        else lw[widx] = bswap32(cur);
+        first = false;
+        ++widx;
+        cur = spill ? c << (32 - spill) : 0u;
+        used = spill;
       }
     }
-    if (used) atomicOr(&lw[widx], bswap32(cur));  // last, partial word: the next block may share it
+    if (used) atomicOr(&lw[widx], bswap32(cur));  // last, partial word: the next lane may share it
   }
   __syncthreads();
-  for (uint32_t i = tid; i < nwords; i += kPackBlocks) {
+  for (uint32_t i = tid; i < nwords; i += 256) {
     const uint32_t v = lw[i];
     if (i == 0 || i == nwords - 1) {
       if (v) atomicOr(&words[w0 + i], v);
@@ -502,7 +525,7 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
                      d_codes_len, codes_cap, d_status);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
                      w.tsum, w.meta, reinterpret_cast<uint32_t *>(d_codes));
-  hipLaunchKernelGGL(enc_pack_kernel, dim3(g256), dim3(256), 0, s, w.sym, w.table, w.blen, w.tsum, nb,
+  hipLaunchKernelGGL(enc_pack_kernel, dim3((uint32_t)((nb + kPackBlocks - 1) / kPackBlocks)), dim3(256), 0, s, w.sym, w.table, w.blen, w.tsum, nb,
                      d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), w.meta);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
