@@ -77,6 +77,28 @@ class EncodedFrame:
     def tables(self) -> tuple[np.ndarray, np.ndarray]:
         return Huffman.generateSplitLookupTables(self.canon)
 
+    def band(self, by0: int, by1: int) -> "EncodedFrame":
+        """Block rows [by0, by1) as a self-contained frame (the
+        single-frame split): blocks are independent given their offsets, so a band
+        needs only the code bytes from its first block's byte to its last block's
+        end. Offsets are rebased to that byte, MH_CODES_PAD zero bytes follow, and
+        the height is the band's pixel rows (the last band keeps the frame's partial
+        block row). Decoding the band gives rows [8*by0, 8*by0 + height) of the frame."""
+        bw, bh = self.block_width, self.block_height
+        if not 0 <= by0 < by1 <= bh:
+            raise ValueError(f"block rows [{by0}, {by1}) outside [0, {bh})")
+        b0, b1 = by0 * bw, by1 * bw
+        offs = self.block_offsets
+        base = int(offs[b0]) >> 3
+        end_bits = int(offs[b1]) if b1 < self.n_blocks else 8 * self.payload_bytes
+        end = (end_bits + 7) >> 3
+        codes = np.zeros(end - base + N.MH_CODES_PAD, np.uint8)
+        codes[: end - base] = self.codes[base:end]
+        band_offs = (offs[b0:b1].astype(np.int64) - 8 * base).astype(np.uint32)
+        init = None if self.block_init is None else self.block_init[b0:b1].copy()
+        height = min(self.height, 8 * by1) - 8 * by0
+        return EncodedFrame(self.width, height, self.canon, codes, band_offs, init, self.flags)
+
 
 class Huffman:
     """Stateless mirror of the reference's `Huffman` class (Shared/Huffman.h)."""

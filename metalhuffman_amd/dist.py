@@ -26,6 +26,17 @@ def shard_range(n_items: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def frame_band(ef, world: int, rank: int):
+    """Single-frame split: `rank`'s contiguous share of the frame's
+    block rows as a self-contained EncodedFrame (EncodedFrame.band) plus its first
+    pixel row. Only that band's code bytes and offsets go to the rank; the decoded
+    bands, stacked in rank order, are the frame."""
+    by0, by1 = shard_range(ef.block_height, world, rank)
+    if by0 == by1:
+        return None, 8 * by0
+    return ef.band(by0, by1), 8 * by0
+
+
 def _bcast_bytes(payload: np.ndarray | None, src: int, device: torch.device, group=None) -> np.ndarray:
     rank = dist.get_rank(group)
     n = torch.zeros(1, dtype=torch.int64, device=device)

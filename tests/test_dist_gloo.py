@@ -87,3 +87,58 @@ def test_gloo_world2_table_broadcast_and_shards():
     assert (lo0, hi0, lo1, hi1) == (0, 4, 4, 7)
     assert ok0 and ok1
     assert tab0 == tab1 == reb0 == reb1      # every rank holds rank 0's T1||T2
+
+
+def _band_worker(rank, world, port, q):
+    """Single-frame split: rank 0 encodes one frame and sends each rank only its
+    band (offsets + code bytes); every rank decodes its rows, rank 0 gathers them."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import metalhuffman_amd as mh
+        from metalhuffman_amd import dist as MD
+        from metalhuffman_amd import frames as F
+        from oracle import oracle as O
+
+        img = np.ascontiguousarray(F.bigbridge()[:777, :1001])
+        bands = [None] * world
+        if rank == 0:
+            ef = mh.encode_frame(img)
+            bands = [MD.frame_band(ef, world, r) for r in range(world)]
+        mine = [None]
+        dist.scatter_object_list(mine, bands if rank == 0 else None, src=0)
+        band, y0 = mine[0]
+        t1, t2 = band.tables()
+        rows = O.decode_frame_shader(band.block_offsets, band.codes, t1, t2, band.width, band.height)
+        got = [None] * world
+        dist.all_gather_object(got, (y0, rows, int(band.codes.size)))
+        full = np.concatenate([g[1] for g in sorted(got, key=lambda g: g[0])])
+        q.put((rank, bool(np.array_equal(full, img)), [g[2] for g in got]))
+    except Exception as e:  # report instead of hanging the peer's queue.get
+        q.put((rank, False, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_single_frame_split():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, ok0, sizes0), (_, ok1, sizes1) = res
+    assert ok0 and ok1, (sizes0, sizes1)
+    assert sizes0 == sizes1 and all(s > 0 for s in sizes0)

@@ -337,3 +337,20 @@ def test_zero_width_windows_match_reference(mh, oracle, device, prepared, flags)
     ref = _oracle_decode(oracle, bad)
     assert not ref.any()
     assert np.array_equal(out[0], ref) and np.array_equal(out[1], ref)
+
+
+@pytest.mark.parametrize("world", [2, 3, 7])
+def test_single_frame_bands(mh, device, bigbridge, world):
+    """Single-frame split: each band, rebased to its own code
+    bytes, decodes on the GPU to exactly its rows of the frame (full BigBridge, a
+    partial-block crop with init bytes)."""
+    from metalhuffman_amd import dist as MD
+    for img, kw in ((bigbridge, {}), (np.ascontiguousarray(bigbridge[:777, :1001]), {"init_zero_delta": True})):
+        ef = mh.encode_frame(img, **kw)
+        rows = []
+        for r in range(world):
+            band, y0 = MD.frame_band(ef, world, r)
+            out = _decode([band], device)[0]
+            assert np.array_equal(out, img[y0: y0 + band.height]), (img.shape, world, r)
+            rows.append(out)
+        assert np.array_equal(np.concatenate(rows), img)
