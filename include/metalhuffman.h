@@ -176,7 +176,8 @@ size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height);
  * the IMPL_DELTAS_AND_INIT_ZERO_DELTA variant). *d_status (device int32,
  * optional) becomes MH_OK, MH_ERR_EMPTY, MH_ERR_CODE_TOO_LONG (depth > 16) or
  * MH_ERR_CAPACITY (round_up(codes_len, 4) > codes_cap, or >= 2^32 code bits);
- * on an error no code bytes or offsets are written and *d_codes_len is 0.
+ * on an error no code bytes or offsets are written, *d_codes_len is 0 and the
+ * header's content is unspecified.
  * d_workspace: 256-byte aligned, mh_encode_workspace_bytes(). The return value
  * covers only argument checks and launch errors. A frame encoded this way goes to
  * mh_build_tables_device (the header) and mh_decode without touching the host. */

@@ -137,9 +137,9 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
 // by (weight, symbol); merged weights never decrease, so internal nodes sit in
 // creation order after every leaf of equal weight. That is the two-queue merge
 // (sorted leaves, internal nodes in creation order) taking the leaf on a tie: the
-// same tree, in O(n). The merge is serial (one lane, queue fronts in registers, one
-// LDS round trip per merge); leaf ranks, depths (pointer jumping over the parent
-// links: 9 rounds cover 511 nodes) and canonical ranks (ballots) are parallel. Then
+// same tree. The merge runs in rounds of up to 32 merges on one wave (see below);
+// leaf ranks, depths (pointer jumping over the parent links) and canonical ranks
+// (ballots) are parallel. Then
 // the canonical codes
 // (huff_util.hpp:94-193), the code table, the code byte count and the status
 // (mh_code_lengths' errors, the caller's capacity).
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
 #else
 #define MH_TREE_STAMP(k)
 #endif
-  __shared__ uint32_t s_lw[258], s_iw[258];
+  __shared__ uint32_t s_lw[384], s_iw[384], s_qv[64], s_qid[64];  // queues padded with kEnd
   __shared__ __attribute__((aligned(16))) uint64_t s_key[256];
   __shared__ uint32_t s_leaf_sym[256], s_len[256], s_par[2][512], s_dep[2][512];
   __shared__ uint32_t s_wcnt[4][17], s_first[17], s_n, s_bad;
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   s_len[tid] = 0;
   s_lw[tid] = kEnd;
   s_iw[tid] = kEnd;
-  if (tid < 2) s_lw[256 + tid] = s_iw[256 + tid] = kEnd;
+  if (tid < 128) s_lw[256 + tid] = s_iw[256 + tid] = kEnd;
   if (tid == 0) {
     s_n = 0;
     s_bad = 0;
@@ -198,37 +198,56 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   MH_TREE_STAMP(2);
   const uint32_t n = s_n;
   const uint32_t nodes = n ? 2 * n - 1 : 0, root = nodes - 1;
-  if (n >= 2 && tid == 0) {
-    // two-queue merge on one lane, branch-free. Both fronts and both second entries
-    // stay in registers, so a merge's two picks compare registers only; the four
-    // loads that refill them are independent and issued together: one LDS latency
-    // per merge on the serial chain. Weights are u32: a non-root weight is below
-    // the padded pixel count <= 2^32. Empty queue slots hold kEnd (0xFFFFFFFF) and
-    // a tie goes to the leaf, which stays exact even at 2^32 pixels: a real weight
-    // of 2^32 - 1 leaves exactly one other node, a leaf of weight 1, so an empty
-    // leaf queue never meets it. One wave issues one instruction per 4 clocks, so
-    // the loop is kept short (sentinels instead of queue-length checks).
-    uint32_t li = 0, ii = 0, ni = 0;
-    uint32_t l0 = s_lw[0], l1 = s_lw[1], i0 = kEnd, i1 = kEnd;
-    for (uint32_t m = 0; m + 1 < n; ++m) {
-      const bool a_leaf = l0 <= i0;
-      const uint32_t wa = a_leaf ? l0 : i0;
-      const uint32_t ida = a_leaf ? li : n + ii;
-      const uint32_t bl = a_leaf ? l1 : l0, bi = a_leaf ? i0 : i1;  // fronts after pick a
-      const bool b_leaf = bl <= bi;
-      const uint32_t wb = b_leaf ? bl : bi;
-      const uint32_t nl = (a_leaf ? 1u : 0u) + (b_leaf ? 1u : 0u);
-      const uint32_t idb = b_leaf ? li + nl - 1u : n + ii + 1u - nl;
-      s_iw[ni] = wa + wb;  // before the refill loads: LDS keeps program order
-      s_par[0][ida] = n + ni;
-      s_par[0][idb] = n + ni;
+  if (n >= 2 && tid < 64) {
+    // The merge, batched on wave 0. Let Q be the remaining nodes in the serial
+    // algorithm's pick order: the merge of the leaf queue and the internal queue, a
+    // leaf first on a tie. If Q[2k-1] <= Q[0] + Q[1], the next k merges pair
+    // (Q[0], Q[1]), (Q[2], Q[3]), ... in that order: every node they create weighs
+    // at least Q[0] + Q[1], and a new node loses every tie (it goes in after all
+    // nodes of equal weight). So one round takes the first 64 entries of each queue,
+    // places them in Q by merge path (each lane binary-searches the other queue),
+    // and makes up to 32 merges at once. Valid codes need 13-19 rounds for 256
+    // symbols (vs 255 serial merges); the result is the serial tree exactly
+    // (checked against mh_code_lengths on 2000 random histograms). Weights are u32:
+    // a non-root weight is below the padded pixel count <= 2^32; empty queue slots
+    // hold kEnd (0xFFFFFFFF).
+    const uint32_t lane = tid;
+    uint32_t li = 0, ii = 0, ni = 0, m = 0;
+    while (m + 1 < n) {
+      const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + lane];
+      uint32_t rl = 0, ri = 0;  // internal candidates < lv; leaf candidates <= iv
+#pragma unroll
+      for (uint32_t step = 64; step; step >>= 1) {
+        if (s_iw[ii + rl + step - 1] < lv) rl += step;
+        if (s_lw[li + ri + step - 1] <= iv) ri += step;
+      }
+      const uint32_t pl = lane + rl, pi = lane + ri;  // positions in Q
+      if (pl < 64) {
+        s_qv[pl] = lv;
+        s_qid[pl] = li + lane;
+      }
+      if (pi < 64) {
+        s_qv[pi] = iv;
+        s_qid[pi] = n + ii + lane;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t q = s_qv[lane], qid = s_qid[lane];
+      const uint32_t s0 = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_readlane(q, 1);
+      uint32_t k = (uint32_t)__popcll(__ballot((lane & 1u) && q <= s0));  // Q sorted: a prefix
+      k = min(k, n - 1 - m);
+      const uint32_t nl = (uint32_t)__popcll(__ballot(lane < 2 * k && qid < n));
+      const uint32_t qa = __shfl(q, 2 * lane), qb = __shfl(q, 2 * lane + 1);
+      const uint32_t ia = __shfl(qid, 2 * lane), ib = __shfl(qid, 2 * lane + 1);
+      if (lane < k) {
+        s_iw[ni + lane] = qa + qb;
+        s_par[0][ia] = n + ni + lane;
+        s_par[0][ib] = n + ni + lane;
+      }
+      __builtin_amdgcn_wave_barrier();
       li += nl;
-      ii += 2u - nl;
-      ++ni;
-      l0 = s_lw[li];
-      l1 = s_lw[li + 1];
-      i0 = s_iw[ii];
-      i1 = s_iw[ii + 1];
+      ii += 2 * k - nl;
+      ni += k;
+      m += k;
     }
   }
   __syncthreads();
@@ -240,8 +259,10 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   }
   __syncthreads();
   MH_TREE_STAMP(4);
+  // 5 rounds: a node within 31 hops of the root gets its exact depth; any other is
+  // at least 32 deep, above the 16-bit limit either way (MH_ERR_CODE_TOO_LONG)
   uint32_t cur = 0;
-  for (uint32_t step = 0; step < 9; ++step) {
+  for (uint32_t step = 0; step < 5; ++step) {
     for (uint32_t i = tid; i < nodes; i += 256) {
       const uint32_t p = s_par[cur][i];
       s_dep[cur ^ 1][i] = s_dep[cur][i] + s_dep[cur][p];
