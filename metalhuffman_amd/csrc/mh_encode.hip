@@ -68,7 +68,10 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
 // row up, histogram into 16 replicated LDS copies (BigBridge-like deltas are mostly
 // one symbol; one copy would serialise every atomic on it). Grid-stride over groups
 // of 32 blocks; one global atomic per used bin per workgroup.
-constexpr uint32_t kHistCopies = 16;
+#ifndef MH_HIST_COPIES
+#define MH_HIST_COPIES 16
+#endif
+constexpr uint32_t kHistCopies = MH_HIST_COPIES;
 #ifndef MH_SPLIT_WGS  // split workgroups: each adds one global atomic per used bin
 #define MH_SPLIT_WGS 256
 #endif
