@@ -29,6 +29,10 @@ namespace {
 
 constexpr uint32_t kScanTile = 256;  // blocks per workgroup in the offsets scan
 constexpr uint32_t kResultBytes = 512;  // mh_encode_frame_device: header, byte count, status
+#ifndef MH_HIST_PARTS
+#define MH_HIST_PARTS 8
+#endif
+constexpr uint32_t kHistParts = MH_HIST_PARTS;  // partial histograms the split workgroups add into
 constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
 
@@ -36,7 +40,7 @@ struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint8_t *sym;       // nb * 64 block symbols
   uint32_t *blen;     // nb per-block bit lengths
   uint32_t *tsum;     // ceil(nb / kScanTile) tile sums (then tile offsets)
-  uint64_t *hist;     // 256 counts
+  uint64_t *hist;     // kHistParts x 256 partial counts
   uint32_t *table;    // 256 x (code_lj16 << 16 | len)
   uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits]]
 };
@@ -53,7 +57,7 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   if (w) w->tsum = reinterpret_cast<uint32_t *>(base + o);
   o += align256(ntiles * 4);
   if (w) w->hist = reinterpret_cast<uint64_t *>(base + o);
-  o += align256(256 * 8);
+  o += align256(kHistParts * 256 * 8);
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
@@ -72,6 +76,10 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
 #define MH_HIST_COPIES 16
 #endif
 constexpr uint32_t kHistCopies = MH_HIST_COPIES;
+#ifndef MH_SPLIT_BATCH  // groups of 32 blocks whose rows a split workgroup loads at once
+#define MH_SPLIT_BATCH 8
+#endif
+constexpr uint32_t kSplitBatch = MH_SPLIT_BATCH;
 #ifndef MH_SPLIT_WGS  // split workgroups: each adds one global atomic per used bin
 #define MH_SPLIT_WGS 256
 #endif
@@ -102,12 +110,10 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
       if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
     return q;
   };
-  uint64_t q_next = load_row(blockIdx.x);
-  for (uint64_t g = blockIdx.x; g * 32 < nb; g += gridDim.x) {
+  // one group of 32 blocks: deltas, init bytes, symbols out, histogram
+  auto process = [&](uint64_t g, uint64_t q) {
     const uint64_t b = g * 32 + (threadIdx.x >> 3);
     const bool on = b < nb;
-    const uint64_t q = q_next;
-    q_next = load_row(g + gridDim.x);  // next group's row in flight while this one is processed
     uint64_t v = q;
     if (delta) {
       // previous pixel: the last pixel of the row above in the same block, 0 for row 0
@@ -126,11 +132,26 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
       reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
     }
+  };
+  // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
+  // flight would leave the frame's read latency-bound
+  const uint64_t ngroups = (nb + 31) / 32;
+  for (uint64_t g0 = blockIdx.x; g0 < ngroups; g0 += (uint64_t)kSplitBatch * gridDim.x) {
+    uint64_t q[kSplitBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = load_row(g0 + (uint64_t)u * gridDim.x);
+#pragma unroll
+    for (uint32_t u = 0; u < kSplitBatch; ++u) {
+      const uint64_t g = g0 + (uint64_t)u * gridDim.x;
+      if (g < ngroups) process(g, q[u]);
+    }
   }
   __syncthreads();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
-  if (c) atomicAdd((unsigned long long *)&hist[threadIdx.x], (unsigned long long)c);
+  // kHistParts partial histograms (workgroups round-robin over them, as over the
+  // XCDs): one address per bin would serialise every workgroup's atomic on it
+  if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
 }
 
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
@@ -163,7 +184,9 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   __shared__ uint32_t s_wcnt[4][17], s_first[17], s_n, s_bad;
   __shared__ unsigned long long s_total;
   const uint32_t tid = threadIdx.x;
-  const uint64_t f = hist[tid];
+  uint64_t f = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kHistParts; ++k) f += hist[k * 256 + tid];
   s_len[tid] = 0;
   s_lw[tid] = kEnd;
   s_iw[tid] = kEnd;
@@ -540,7 +563,7 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const uint64_t ntiles = (nb + kScanTile - 1) / kScanTile;
   if (g256 == 0 || ntiles > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
 
-  if (hipMemsetAsync(w.hist, 0, 256 * 8, s) != hipSuccess) return MH_ERR_HIP;
+  if (hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess) return MH_ERR_HIP;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
   const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, MH_SPLIT_WGS);
   hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
