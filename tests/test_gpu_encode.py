@@ -153,3 +153,30 @@ def test_async_encode_errors_write_nothing(mh, device):
     torch.cuda.synchronize(device)
     assert int(b.status.item()) == -4 and int(b.codes_len.item()) == 0
     assert bool((small == 0xCD).all())
+
+
+def test_async_encode_many_frames_back_to_back(mh, device, bigbridge):
+    """Frames enqueued back to back on one workspace (the scan's completion ticket and
+    the histograms are reused every call), then on two streams with one encoder each:
+    every frame byte-identical to the host codec."""
+    import torch
+    from metalhuffman_amd import frames as F
+    from metalhuffman_amd.encoder import Encoder
+    h, w = 512, 768
+    imgs = [np.ascontiguousarray(F.block_shuffle(bigbridge, 40 + k)[:h, :w]) for k in range(24)]
+    hosts = [mh.encode_frame(im) for im in imgs]
+    dimgs = [torch.from_numpy(im).to(device) for im in imgs]
+    enc = Encoder(w, h, device)
+    outs = [enc.encode_async(d) for d in dimgs]
+    encs = [Encoder(w, h, device) for _ in range(2)]
+    streams = [torch.cuda.Stream(device) for _ in range(2)]
+    for st in streams:  # the frames were uploaded on the current stream
+        st.wait_stream(torch.cuda.current_stream(device))
+    outs2 = [encs[k % 2].encode_async(d, stream=streams[k % 2]) for k, d in enumerate(dimgs)]
+    torch.cuda.synchronize(device)
+    for o, o2, ref in zip(outs, outs2, hosts):
+        for a in (o, o2):
+            r = a.result()
+            assert np.array_equal(r.canon, ref.canon)
+            assert np.array_equal(r.codes.cpu().numpy(), ref.codes)
+            assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)
