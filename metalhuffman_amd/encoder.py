@@ -79,8 +79,9 @@ class Encoder:
                      stream: Optional[torch.cuda.Stream] = None,
                      codes: Optional[torch.Tensor] = None) -> AsyncEncodedFrame:
         """Enqueue the encode on `stream` (default: the current stream) and return
-        at once. `codes` may be a reused u8 buffer of at least the encoder's
-        capacity (the default allocates one)."""
+        at once. `gray` must be ready on that stream (make it wait on the stream
+        that produced the frame). `codes` may be a reused u8 buffer of at least the
+        encoder's capacity (the default allocates one)."""
         if gray.dtype != torch.uint8 or gray.shape != (self.height, self.width) or not gray.is_contiguous():
             raise ValueError(f"gray must be contiguous uint8 [{self.height}, {self.width}]")
         if gray.device != self.device:
