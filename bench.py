@@ -325,7 +325,14 @@ def encode_rate(device, bb, reps=32):
     for k in range(4):
         mh.encode_frame(imgs[k])
     cpu_s = (time.perf_counter() - t0) / 4
+    # algorithmic bytes of one encode: pixels in, code bytes + block offsets out (the
+    # block-symbol intermediate is not counted: it is the encoder's own choice)
+    ref = mh.encode_frame(imgs[0])
+    alg = bb.size + ref.codes.size + 4 * ref.n_blocks
     return {"gpu_ms_per_frame": round(gpu_s * 1e3, 3), "gpu_MBps": round(bb.size / gpu_s / 1e6, 1),
+            "algorithmic_bytes_per_frame": int(alg),
+            "gpu_async_2streams_algorithmic_GBps": round(alg / pipe_s / 1e9, 1),
+            "gpu_async_2streams_frac_of_8TBps": round(alg / pipe_s / 8e12, 4),
             "gpu_async_ms_per_frame": round(async_s * 1e3, 3),
             "gpu_async_MBps": round(bb.size / async_s / 1e6, 1),
             "gpu_async_2streams_ms_per_frame": round(pipe_s * 1e3, 3),
