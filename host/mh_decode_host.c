@@ -13,6 +13,11 @@
  *       buffers exactly as the reference encoder emits them (256-byte canonical
  *       header, MSB-first codes, u32 LE block bit offsets -- HuffmanUtil.cpp:
  *       1051-1131) decoded unchanged and compared with the expected pixels.
+ *   mh_decode_host device W H [reps]
+ *       the whole chain on the GPU with no host round trip: the frame is encoded
+ *       on the device (mh_encode_frame_device_async), the tables are built from
+ *       the device header (mh_build_tables_device), then mh_decode; the encoded
+ *       bytes are compared with the host codec's and the raster with the frame.
  *
  * Prints one line "decode ok W H ..." (exit 0) or the first mismatch (exit 1).
  */
@@ -80,11 +85,131 @@ static void synth_frame(uint8_t *img, uint32_t w, uint32_t h) {
     }
 }
 
+/* encode -> tables -> decode, all on the device (the producer and the consumer of
+ * the reference's buffers on one GPU, nothing through the host in between) */
+static int device_chain(uint32_t w, uint32_t h, int reps) {
+  const uint32_t bw = (w + 7) / 8, bh = (h + 7) / 8, nb = bw * bh;
+  const size_t pitch = ((size_t)w + 7) & ~(size_t)7;
+  uint8_t *img = (uint8_t *)xmalloc((size_t)w * h);
+  synth_frame(img, w, h);
+  /* the host codec's bytes, to compare with */
+  const uint64_t cap = mh_codes_bound((uint64_t)nb * 64) + MH_CODES_PAD + 4;
+  uint8_t canon[256], *codes = (uint8_t *)xmalloc(cap);
+  uint32_t *offsets = (uint32_t *)xmalloc((size_t)nb * 4);
+  uint64_t codes_len = 0;
+  MH_OK_OR_DIE(mh_encode_frame(img, w, h, 0, canon, codes, cap, &codes_len, offsets, NULL));
+
+  uint8_t *d_gray, *d_codes, *d_canon, *d_out, *d_ws;
+  uint32_t *d_offsets, *d_t2_entries;
+  uint64_t *d_codes_len;
+  int32_t *d_status;
+  mh_lookup_symbol *d_t1, *d_t2;
+  uint16_t *d_lut;
+  const size_t ws = mh_encode_workspace_bytes(w, h);
+  HIP_OK(hipMalloc((void **)&d_gray, (size_t)w * h));
+  HIP_OK(hipMalloc((void **)&d_codes, cap));
+  HIP_OK(hipMalloc((void **)&d_canon, 256));
+  HIP_OK(hipMalloc((void **)&d_out, pitch * h));
+  HIP_OK(hipMalloc((void **)&d_ws, ws));
+  HIP_OK(hipMalloc((void **)&d_offsets, (size_t)nb * 4));
+  HIP_OK(hipMalloc((void **)&d_t2_entries, 4));
+  HIP_OK(hipMalloc((void **)&d_codes_len, 8));
+  HIP_OK(hipMalloc((void **)&d_status, 8));
+  HIP_OK(hipMalloc((void **)&d_t1, 256 * sizeof(mh_lookup_symbol)));
+  HIP_OK(hipMalloc((void **)&d_t2, MH_TABLE2_MAX_ENTRIES * sizeof(mh_lookup_symbol)));
+  HIP_OK(hipMalloc((void **)&d_lut, mh_lut_bytes()));
+  HIP_OK(hipMemcpy(d_gray, img, (size_t)w * h, hipMemcpyHostToDevice));
+
+  mh_frame fr;
+  memset(&fr, 0, sizeof(fr));
+  fr.d_block_offsets = d_offsets;
+  fr.d_codes = d_codes;
+  fr.codes_bytes = cap; /* the byte count stays on the device: the decoder bounds blocks by offsets */
+  fr.d_table1 = d_t1;
+  fr.d_table2 = d_t2;
+  fr.table2_entries = MH_TABLE2_MAX_ENTRIES;
+  fr.d_lut = d_lut;
+  fr.dims.width = w;
+  fr.dims.height = h;
+  fr.dims.block_width = bw;
+  fr.dims.block_height = bh;
+  fr.n_frames = 1;
+
+#define CHAIN()                                                                                      \
+  do {                                                                                               \
+    MH_OK_OR_DIE(mh_encode_frame_device_async(d_gray, w, h, 0, d_canon, d_codes, cap, d_codes_len,   \
+                                              d_offsets, NULL, d_status, d_ws, ws, NULL));           \
+    MH_OK_OR_DIE(mh_build_tables_device(d_canon, d_t1, d_t2, d_t2_entries, d_lut, d_status + 1, NULL)); \
+    MH_OK_OR_DIE(mh_decode(&fr, d_out, pitch, pitch * h, NULL));                                     \
+  } while (0)
+  CHAIN();
+  HIP_OK(hipDeviceSynchronize());
+  int32_t status[2];
+  uint64_t dev_len = 0;
+  uint8_t dev_canon[256];
+  HIP_OK(hipMemcpy(status, d_status, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&dev_len, d_codes_len, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(dev_canon, d_canon, 256, hipMemcpyDeviceToHost));
+  if (status[0] != MH_OK || status[1] != MH_OK) {
+    printf("device status %d %d\n", status[0], status[1]);
+    return 1;
+  }
+  uint8_t *dev_codes = (uint8_t *)xmalloc(codes_len);
+  uint32_t *dev_offsets = (uint32_t *)xmalloc((size_t)nb * 4);
+  HIP_OK(hipMemcpy(dev_codes, d_codes, codes_len, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(dev_offsets, d_offsets, (size_t)nb * 4, hipMemcpyDeviceToHost));
+  if (dev_len != codes_len || memcmp(dev_canon, canon, 256) || memcmp(dev_codes, codes, codes_len) ||
+      memcmp(dev_offsets, offsets, (size_t)nb * 4)) {
+    printf("ENCODE MISMATCH: device %llu bytes vs host %llu\n", (unsigned long long)dev_len,
+           (unsigned long long)codes_len);
+    return 1;
+  }
+  uint8_t *got = (uint8_t *)xmalloc(pitch * h);
+  HIP_OK(hipMemcpy(got, d_out, pitch * h, hipMemcpyDeviceToHost));
+  for (uint32_t y = 0; y < h; ++y)
+    for (uint32_t x = 0; x < w; ++x)
+      if (got[(size_t)y * pitch + x] != img[(size_t)y * w + x]) {
+        printf("MISMATCH at x=%u y=%u\n", x, y);
+        return 1;
+      }
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, NULL));
+  for (int i = 0; i < reps; ++i) CHAIN();
+  HIP_OK(hipEventRecord(e1, NULL));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+#undef CHAIN
+  printf("device ok %u %u codes_bytes %llu us_per_encode_tables_decode %.2f\n", w, h,
+         (unsigned long long)codes_len, reps > 0 ? 1e3 * ms / reps : 0.0);
+  hipFree(d_gray);
+  hipFree(d_codes);
+  hipFree(d_canon);
+  hipFree(d_out);
+  hipFree(d_ws);
+  hipFree(d_offsets);
+  hipFree(d_t2_entries);
+  hipFree(d_codes_len);
+  hipFree(d_status);
+  hipFree(d_t1);
+  hipFree(d_t2);
+  hipFree(d_lut);
+  free(img);
+  free(codes);
+  free(offsets);
+  free(dev_codes);
+  free(dev_offsets);
+  free(got);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc < 4) {
     fprintf(stderr,
             "usage: %s synth W H [reps] | raw W H file.gray [reps] |\n"
-            "       buffers W H canon.bin codes.bin offsets.bin expected.gray\n",
+            "       buffers W H canon.bin codes.bin offsets.bin expected.gray | device W H [reps]\n",
             argv[0]);
     return 2;
   }
@@ -92,6 +217,7 @@ int main(int argc, char **argv) {
   const uint32_t w = (uint32_t)strtoul(argv[2], NULL, 10), h = (uint32_t)strtoul(argv[3], NULL, 10);
   const uint32_t bw = (w + 7) / 8, bh = (h + 7) / 8, nb = bw * bh;
   int reps = 20;
+  if (!strcmp(mode, "device")) return device_chain(w, h, argc > 4 ? atoi(argv[4]) : 20);
 
   uint8_t canon[256];
   uint8_t *codes = NULL, *expected = NULL;

@@ -68,3 +68,13 @@ def test_host_reference_encoder_buffers(host_bin, tmp_path):
         assert r.stdout.startswith(f"decode ok {w} {h} "), (name, r.stdout)
         n += 1
     assert n >= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wh", [(2048, 1536), (1001, 777), (13, 5)])
+def test_host_device_chain(host_bin, wh):
+    """encode -> tables -> decode on the device through the C-ABI only: the device
+    encoder's bytes equal the host codec's and the raster equals the frame."""
+    r = _run([host_bin, "device", str(wh[0]), str(wh[1]), "5"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith(f"device ok {wh[0]} {wh[1]} "), r.stdout
