@@ -34,7 +34,7 @@ SOURCES = {
                                       "-Wall", "-c"]),
     "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),
 }
-HEADERS = [os.path.join(ROOT, "include", "metalhuffman.h")]
+HEADERS = [os.path.join(ROOT, "include", "metalhuffman.h"), os.path.join(CSRC, "mh_lut.hpp")]
 
 
 def _stale(target: str, deps: list[str]) -> bool:

@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "../../include/metalhuffman.h"
+#include "mh_lut.hpp"
 
 namespace {
 
@@ -73,27 +74,9 @@ namespace {
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
-constexpr int kLutBits = 13;                  // first-level index width
-constexpr int kL1Entries = 1 << kLutBits;     // 8192 x u16
-constexpr int kL2Bits = 16 - kLutBits;        // 3 more window bits for long codes
-constexpr int kL2Subtables = 129;             // dummy + <=128 long-code prefixes
-constexpr int kL2Entries = kL2Subtables << kL2Bits;      // 1032
-constexpr int kLutEntries = kL1Entries + 1040;           // L1 + L2, padded to 16 B
-constexpr int kLutBytes = kLutEntries * 2;               // 18464: the 13-bit table
-// The prepared table buffer (mh_prepare_lut) also holds a single-level 14-bit
-// table (no escapes; valid when no code exceeds 14 bits) and the longest code
-// length, for the small-launch kernel.
-constexpr int kLut14Bits = 14;
-constexpr int kLut14Entries = 1 << kLut14Bits;           // 16384 x u16
-constexpr int kLut14Off = kLutBytes;                     // byte offset in the buffer
-constexpr int kLut14Bytes = kLut14Entries * 2;           // 32768
-constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest, u32 shortest code length
-constexpr int kPreparedBytes = kMaxLenOff + 16;          // 51248
 constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile span)
 constexpr int kMaxWavesPerWG = MH_MAX_WAVES;
-static_assert(kLutBytes % 16 == 0 && kLut14Bytes % 16 == 0, "lut copy uses 16-byte chunks");
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
-static_assert(kL2Subtables < 240, "escape entries must stay below the smallest step word");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
@@ -132,19 +115,6 @@ __device__ __forceinline__ uint32_t split_lookup(const uint16_t *t1, const uint1
   return e;
 }
 
-// LUT entry format ("step word"): a valid {symbol, bitWidth} becomes
-//   E = (symbol << 8) - bitWidth  (mod 2^16),
-// so ONE add of E to the lane state S (see decode_block) advances the bit cursor
-// (low byte) and folds the delta into prev (byte 1). Valid entries have a low
-// byte in [240, 255] (bitWidth 1..16), so E >= 240. Escapes to the second level
-// are E = sub < 129, and a window the table does not decode ({0,0} in the
-// reference) is E = 0: adding it changes nothing, exactly the reference's
-// zero-width step.
-__device__ __forceinline__ uint32_t step_word(uint32_t e) {
-  const uint32_t len = e >> 8;
-  return len ? (((e & 0xFFu) << 8) - len) & 0xFFFFu : 0u;
-}
-constexpr uint32_t kEscapeBelow = 240u;
 
 // Builds the two-level table into `lut` (LDS or global) with `nthreads`
 // cooperating threads; `p0` is a scratch word shared by them.
@@ -182,38 +152,16 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
   sync();
 }
 
-// Single-level 14-bit table: step_word of every window whose code has <= 14 bits
-// (0 otherwise), and the longest code length of the table into *max_len.
-__device__ void build_lut14(const uint16_t *t1, const uint16_t *t2, uint32_t t2_entries,
-                            uint16_t *lut14, uint32_t *max_len, uint32_t *min_len, uint32_t tid,
-                            uint32_t nthreads) {
-  uint32_t mx = 0, mn = 255;
-  for (uint32_t p = tid; p < (uint32_t)kLut14Entries; p += nthreads) {
-    const uint32_t e = split_lookup(t1, t2, t2_entries, p << (16 - kLut14Bits));
-    const uint32_t len = e >> 8;
-    lut14[p] = (uint16_t)(len <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
-    mx = max(mx, len);
-    if (len) mn = min(mn, len);
-  }
-  atomicMax(max_len, mx);
-  atomicMin(min_len, mn);
-}
 
+// mh_prepare_lut: the prepared tables from T1/T2 in device memory, one workgroup
+// (build_prepared_lut, mh_lut.hpp).
 __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1, const uint16_t *t2,
                                                               uint32_t t2_entries, uint8_t *buf) {
-  __shared__ uint32_t p0, mx, mn;
-  if (threadIdx.x == 0) {
-    mx = 0;
-    mn = 255;
-  }
-  build_lut(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf), &p0, threadIdx.x, blockDim.x,
-            [] { __syncthreads(); });
-  build_lut14(t1, t2, t2_entries, reinterpret_cast<uint16_t *>(buf + kLut14Off), &mx, &mn, threadIdx.x,
-              blockDim.x);
+  __shared__ uint16_t s_t1[256];
+  __shared__ uint32_t s_scratch[3];
+  if (threadIdx.x < 256) s_t1[threadIdx.x] = t1[threadIdx.x];
   __syncthreads();
-  // [longest code, shortest code, 0, 0]
-  if (threadIdx.x < 4)
-    reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[threadIdx.x] = threadIdx.x == 0 ? mx : threadIdx.x == 1 ? mn : 0u;
+  build_prepared_lut(s_t1, t2, t2_entries, buf, s_scratch);
 }
 
 // Word source for the bit cursor: big-endian dwords of the tile's code span.

@@ -13,43 +13,63 @@
 //                    T2[group*256 + lo] = {symbol, len}; T2 subtable 0 is all zero.
 // For a header whose code lengths form a prefix code (every encoder output), each
 // table slot is written by at most one symbol, so one thread per symbol fills its
-// range without ordering concerns. Headers that are not prefix codes (Kraft sum
+// range without ordering concerns. Everything is built in LDS (T2's whole capacity,
+// 131.5 KB, fits gfx950's LDS) and written out once. Headers that are not prefix codes (Kraft sum
 // > 1) or hold a length > 16 are rejected with a status word.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
 #include "../../include/metalhuffman.h"
+#include "mh_lut.hpp"
 
 namespace {
 
+// Every workgroup builds T1 and T2 (T2's whole capacity) in LDS; workgroup 0 writes
+// them out with 16-byte stores, and -- when `lut` is given -- each workgroup then
+// fills its slice of the decoder's prepared table straight from its LDS copies
+// (the same entries as mh_prepare_lut over the written tables, tests/test_gpu_tables.py):
+// the prepared table's ~25 K entries are spread over the grid instead of one CU.
+// P0 (the first 13-bit prefix of a code longer than 13 bits) and the longest /
+// shortest code words come from the canonical codes themselves, so the slices need
+// no exchange. Launch: kTableGroups workgroups of 1024 threads.
+constexpr uint32_t kTableGroups = 32;
 __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *canon, uint16_t *t1,
                                                                uint16_t *t2, uint32_t *t2_entries,
-                                                               int32_t *status) {
-  __shared__ uint32_t s_len[256], s_code[256], s_mark[256], s_group[256];
-  __shared__ uint32_t s_cnt[17], s_first[17], s_kraft, s_bad, s_ngroups;
-  const uint32_t tid = threadIdx.x;
+                                                               int32_t *status, uint8_t *lut) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_t2[MH_TABLE2_MAX_ENTRIES];
+  __shared__ __attribute__((aligned(16))) uint16_t s_t1[256];
+  __shared__ uint32_t s_group[256], s_wcnt[4][17], s_gcnt[4];
+  __shared__ uint32_t s_first[17], s_kraft, s_bad, s_ngroups, s_mx, s_mn;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  static_assert(MH_TABLE2_MAX_ENTRIES % 8 == 0, "16-byte copies");
+  constexpr uint32_t kT2Vec = MH_TABLE2_MAX_ENTRIES / 8;
 
-  for (uint32_t i = tid; i < (uint32_t)MH_TABLE2_MAX_ENTRIES; i += blockDim.x) t2[i] = 0;
+  uint4 *s_t2v = reinterpret_cast<uint4 *>(s_t2);
+  for (uint32_t i = tid; i < kT2Vec; i += blockDim.x) s_t2v[i] = make_uint4(0, 0, 0, 0);
+  const uint32_t L = tid < 256 ? canon[tid] : 0u;
   if (tid < 256) {
-    t1[tid] = 0;
-    s_len[tid] = canon[tid];
-    s_mark[tid] = 0;
+    s_t1[tid] = 0;
+    s_group[tid] = 0;
   }
-  if (tid < 17) s_cnt[tid] = 0;
   if (tid == 0) {
     s_kraft = 0;
     s_bad = 0;
+    s_mx = 0;
+    s_mn = 255;
   }
   __syncthreads();
-
-  const uint32_t L = tid < 256 ? s_len[tid] : 0u;
-  if (tid < 256 && L) {
-    if (L > 16) {
-      atomicOr(&s_bad, 1u);
-    } else {
-      atomicAdd(&s_cnt[L], 1u);
-      atomicAdd(&s_kraft, 1u << (16 - L));
+  // codes per length and each symbol's rank among equal lengths (symbol order):
+  // one ballot per length per wave
+  uint32_t in_wave = 0;
+  if (tid < 256) {
+    if (L > 16) atomicOr(&s_bad, 1u);
+    else if (L) atomicAdd(&s_kraft, 1u << (16 - L));
+    for (uint32_t l = 1; l <= 16; ++l) {
+      const uint64_t m = __ballot(L == l);
+      if (L == l) in_wave = (uint32_t)__popcll(m & below);
+      if (lane == 0) s_wcnt[wave][l] = (uint32_t)__popcll(m);
     }
   }
   __syncthreads();
@@ -58,50 +78,114 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     uint32_t code = 0;
     for (uint32_t l = 1; l <= 16; ++l) {
       s_first[l] = code;
-      code = (code + s_cnt[l]) << 1;
+      code = (code + s_wcnt[0][l] + s_wcnt[1][l] + s_wcnt[2][l] + s_wcnt[3][l]) << 1;
     }
     if (s_kraft > 65536u) s_bad |= 2u;
   }
   __syncthreads();
-  if (s_bad) {
-    if (tid == 0) {
-      *t2_entries = 256;
-      if (status) *status = (s_bad & 1u) ? MH_ERR_CODE_TOO_LONG : MH_ERR_TABLE;
+  const bool bad = s_bad != 0;  // rejected: the tables stay all zero
+  uint32_t code = 0;
+  if (!bad && tid < 256 && L) {
+    uint32_t rank = in_wave;  // symbols of the same length before this one
+    for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
+    code = ((s_first[L] + rank) << (16 - L)) & 0xFFFFu;
+    // longest / shortest code as mh_prepare_lut samples them (windows at multiples
+    // of 4): a code of <= 14 bits always holds one, a 15/16-bit code iff it starts there
+    if (L <= 14 || (code & 3u) == 0) {
+      atomicMax(&s_mx, L);
+      atomicMin(&s_mn, L);
     }
-    return;
   }
-
-  if (tid < 256 && L) {
-    uint32_t rank = 0;  // symbols of the same length before this one
-    for (uint32_t s = 0; s < tid; ++s) rank += s_len[s] == L ? 1u : 0u;
-    const uint32_t code = ((s_first[L] + rank) << (16 - L)) & 0xFFFFu;
-    s_code[tid] = code;
-    if (L > 8) s_mark[code >> 8] = 1;
+  // long codes grouped by high byte, groups numbered 1.. in ascending high-byte order
+  if (!bad && tid < 256 && L > 8) s_group[code >> 8] = 1;  // (every writer of a slot stores 1)
+  __syncthreads();
+  uint32_t mark = 0, gpre = 0;
+  if (tid < 256) {
+    mark = s_group[tid];
+    const uint64_t m = __ballot(mark != 0);
+    gpre = (uint32_t)__popcll(m & below);
+    if (lane == 0) s_gcnt[wave] = (uint32_t)__popcll(m);
   }
   __syncthreads();
   if (tid < 256) {
-    uint32_t g = 0;
-    for (uint32_t h = 0; h < tid; ++h) g += s_mark[h];
-    s_group[tid] = s_mark[tid] ? g + 1u : 0u;
-    if (tid == 255) s_ngroups = g + s_mark[255];
+    uint32_t g = gpre;
+    for (uint32_t w = 0; w < wave; ++w) g += s_gcnt[w];
+    s_group[tid] = mark ? g + 1u : 0u;
+    if (tid == 255) s_ngroups = g + mark;
   }
   __syncthreads();
-
-  if (tid < 256 && L) {
-    const uint32_t code = s_code[tid];
+  if (!bad && tid < 256 && L) {
     const uint16_t e = (uint16_t)(tid | (L << 8));
     if (L <= 8) {
-      for (uint32_t i = 0; i < (1u << (8 - L)); ++i) t1[(code >> 8) + i] = e;
+      for (uint32_t i = 0; i < (1u << (8 - L)); ++i) s_t1[(code >> 8) + i] = e;
     } else {
-      uint16_t *sub = t2 + s_group[code >> 8] * 256u;
-      for (uint32_t i = 0; i < (1u << (16 - L)); ++i) sub[(code & 0xFFu) + i] = e;
+      uint16_t *sub = s_t2 + s_group[code >> 8] * 256u + (code & 0xFFu);
+      for (uint32_t i = 0; i < (1u << (16 - L)); ++i) sub[i] = e;
     }
   }
   __syncthreads();  // (valid prefix code: a group's high byte carries no short code)
-  if (tid < 256 && s_group[tid]) t1[tid] = (uint16_t)s_group[tid];
-  if (tid == 0) {
-    *t2_entries = (s_ngroups + 1u) * 256u;
-    if (status) *status = MH_OK;
+  if (tid < 256 && s_group[tid]) s_t1[tid] = (uint16_t)s_group[tid];
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    // out: T1, T2 over its whole capacity (zero past the used subtables)
+    if (((uintptr_t)t1 & 15u) == 0) {
+      if (tid < 32) reinterpret_cast<uint4 *>(t1)[tid] = reinterpret_cast<const uint4 *>(s_t1)[tid];
+    } else if (tid < 256) {
+      t1[tid] = s_t1[tid];
+    }
+    if (((uintptr_t)t2 & 15u) == 0) {
+      uint4 *v = reinterpret_cast<uint4 *>(t2);
+      for (uint32_t i = tid; i < kT2Vec; i += blockDim.x) v[i] = s_t2v[i];
+    } else {
+      for (uint32_t i = tid; i < (uint32_t)MH_TABLE2_MAX_ENTRIES; i += blockDim.x) t2[i] = s_t2[i];
+    }
+    if (tid == 0) {
+      *t2_entries = bad ? 256u : (s_ngroups + 1u) * 256u;
+      if (status) *status = bad ? ((s_bad & 1u) ? MH_ERR_CODE_TOO_LONG : MH_ERR_TABLE) : MH_OK;
+    }
+    if (lut && tid < 4)  // [longest code, shortest code, 0, 0]
+      reinterpret_cast<uint32_t *>(lut + kMaxLenOff)[tid] = tid == 0 ? s_mx : tid == 1 ? s_mn : 0u;
+  }
+  if (!lut) return;
+  // this workgroup's slice of the prepared entries: L1 | L2 | the 14-bit table
+  uint32_t lmin = 0;  // shortest code length above 13 bits, 0 if none
+  for (uint32_t l = 16; l > (uint32_t)kLutBits; --l)
+    if (s_wcnt[0][l] + s_wcnt[1][l] + s_wcnt[2][l] + s_wcnt[3][l]) lmin = l;
+  const uint32_t P0 = (!bad && lmin) ? (((s_first[lmin] << (16 - lmin)) & 0xFFFFu) >> kL2Bits)
+                                     : (uint32_t)kL1Entries;
+  const uint32_t nl2 = ((uint32_t)kL1Entries - P0) << kL2Bits;
+  constexpr uint32_t kL2Region = (uint32_t)(kLutEntries - kL1Entries);
+  constexpr uint32_t kAll = (uint32_t)kL1Entries + kL2Region + (uint32_t)kLut14Entries;
+  const uint32_t per = (kAll + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = blockIdx.x * per, hi = min(kAll, lo + per);
+  uint16_t *out = reinterpret_cast<uint16_t *>(lut);
+  uint16_t *out14 = reinterpret_cast<uint16_t *>(lut + kLut14Off);
+  auto lookup = [&](uint32_t pat16) -> uint32_t {
+    uint32_t e = s_t1[pat16 >> 8];
+    if ((e >> 8) == 0) e = s_t2[(e & 0xFFu) * 256u + (pat16 & 0xFFu)];
+    return e;
+  };
+  for (uint32_t v = lo + tid; v < hi; v += blockDim.x) {
+    if (v < (uint32_t)kL1Entries) {
+      const uint32_t p = v;
+      uint32_t w;
+      if (p >= P0) {
+        const uint32_t sub = p - P0 + 1;
+        w = sub < (uint32_t)kL2Subtables ? sub : 0u;
+      } else {
+        w = step_word(lookup(p << kL2Bits));
+      }
+      out[p] = (uint16_t)w;
+    } else if (v < (uint32_t)kL1Entries + kL2Region) {
+      const uint32_t i = v - (uint32_t)kL1Entries;  // L2 subtable 0 and the padding stay zero
+      const uint32_t j = i - (1u << kL2Bits);
+      const bool live = i >= (1u << kL2Bits) && j < nl2 && j < (uint32_t)(kL2Entries - (1 << kL2Bits));
+      out[kL1Entries + i] = (uint16_t)(live ? step_word(lookup((P0 << kL2Bits) + j)) : 0u);
+    } else {
+      const uint32_t q = v - (uint32_t)kL1Entries - kL2Region;
+      const uint32_t e = lookup(q << (16 - kLut14Bits));
+      out14[q] = (uint16_t)((e >> 8) <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
+    }
   }
 }
 
@@ -113,10 +197,8 @@ extern "C" int mh_build_tables_device(const uint8_t *d_canon_header, mh_lookup_s
   if (!d_canon_header || !d_table1 || !d_table2 || !d_table2_entries) return MH_ERR_INVALID_ARG;
   if ((uintptr_t)d_lut & 15u) return MH_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(mh_build_tables_kernel, dim3(1), dim3(1024), 0, s, d_canon_header,
+  hipLaunchKernelGGL(mh_build_tables_kernel, dim3(d_lut ? kTableGroups : 1), dim3(1024), 0, s, d_canon_header,
                      reinterpret_cast<uint16_t *>(d_table1), reinterpret_cast<uint16_t *>(d_table2),
-                     d_table2_entries, d_status);
-  if (hipGetLastError() != hipSuccess) return MH_ERR_HIP;
-  // The prepared table reads T2 through its full (zero-padded) capacity.
-  return d_lut ? mh_prepare_lut(d_table1, d_table2, MH_TABLE2_MAX_ENTRIES, d_lut, stream) : MH_OK;
+                     d_table2_entries, d_status, reinterpret_cast<uint8_t *>(d_lut));
+  return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
