@@ -881,7 +881,11 @@ int mh_diag_stamps(unsigned long long *host, size_t n) {
 }
 #endif
 
+#ifdef MH_TABLE_STAMPS  // diagnostic builds: room for the table kernel's phase stamps
+size_t mh_lut_bytes(void) { return (size_t)kPreparedBytes + 256; }
+#else
 size_t mh_lut_bytes(void) { return (size_t)kPreparedBytes; }
+#endif
 int mh_lut_bits(void) { return kLutBits; }
 
 int mh_device_count(void) {

@@ -25,8 +25,8 @@
 
 namespace {
 
-// Every workgroup builds T1 and T2 (T2's whole capacity) in LDS; workgroup 0 writes
-// them out with 16-byte stores, and -- when `lut` is given -- each workgroup then
+// Every workgroup builds T1 and the used part of T2 in LDS; workgroup 0 writes them
+// out with 16-byte stores (T2 zero-padded to its whole capacity), and -- when `lut` is given -- each workgroup then
 // fills its slice of the decoder's prepared table straight from its LDS copies
 // (the same entries as mh_prepare_lut over the written tables, tests/test_gpu_tables.py):
 // the prepared table's ~25 K entries are spread over the grid instead of one CU.
@@ -42,12 +42,18 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
   __shared__ uint32_t s_group[256], s_wcnt[4][17], s_gcnt[4];
   __shared__ uint32_t s_first[17], s_kraft, s_bad, s_ngroups, s_mx, s_mn;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+#ifdef MH_TABLE_STAMPS
+#define TAB_STAMP(i) \
+  if (lut && blockIdx.x == 0 && tid == 0) reinterpret_cast<uint64_t *>(lut + kPreparedBytes)[i] = __builtin_amdgcn_s_memtime();
+  TAB_STAMP(0);
+#else
+#define TAB_STAMP(i)
+#endif
   const uint64_t below = (1ull << lane) - 1ull;
   static_assert(MH_TABLE2_MAX_ENTRIES % 8 == 0, "16-byte copies");
   constexpr uint32_t kT2Vec = MH_TABLE2_MAX_ENTRIES / 8;
 
   uint4 *s_t2v = reinterpret_cast<uint4 *>(s_t2);
-  for (uint32_t i = tid; i < kT2Vec; i += blockDim.x) s_t2v[i] = make_uint4(0, 0, 0, 0);
   const uint32_t L = tid < 256 ? canon[tid] : 0u;
   if (tid < 256) {
     s_t1[tid] = 0;
@@ -60,6 +66,7 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     s_mn = 255;
   }
   __syncthreads();
+  TAB_STAMP(1);
   // codes per length and each symbol's rank among equal lengths (symbol order):
   // one ballot per length per wave
   uint32_t in_wave = 0;
@@ -73,6 +80,7 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     }
   }
   __syncthreads();
+  TAB_STAMP(2);
   if (tid == 0) {
     // first code of each length: shift left across every length step
     uint32_t code = 0;
@@ -83,22 +91,33 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     if (s_kraft > 65536u) s_bad |= 2u;
   }
   __syncthreads();
+  TAB_STAMP(3);
   const bool bad = s_bad != 0;  // rejected: the tables stay all zero
   uint32_t code = 0;
   if (!bad && tid < 256 && L) {
     uint32_t rank = in_wave;  // symbols of the same length before this one
     for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
     code = ((s_first[L] + rank) << (16 - L)) & 0xFFFFu;
+  }
+  {
     // longest / shortest code as mh_prepare_lut samples them (windows at multiples
-    // of 4): a code of <= 14 bits always holds one, a 15/16-bit code iff it starts there
-    if (L <= 14 || (code & 3u) == 0) {
-      atomicMax(&s_mx, L);
-      atomicMin(&s_mn, L);
+    // of 4): a code of <= 14 bits always holds one, a 15/16-bit code iff it starts
+    // there. Wave reductions first: 256 LDS atomics on one word serialise.
+    const bool seen = !bad && tid < 256 && L && (L <= 14 || (code & 3u) == 0);
+    uint32_t vmx = seen ? L : 0u, vmn = seen ? L : 255u;
+    for (uint32_t o = 32; o; o >>= 1) {
+      vmx = max(vmx, (uint32_t)__shfl_xor(vmx, o));
+      vmn = min(vmn, (uint32_t)__shfl_xor(vmn, o));
+    }
+    if (tid < 256 && lane == 0) {
+      atomicMax(&s_mx, vmx);
+      atomicMin(&s_mn, vmn);
     }
   }
   // long codes grouped by high byte, groups numbered 1.. in ascending high-byte order
   if (!bad && tid < 256 && L > 8) s_group[code >> 8] = 1;  // (every writer of a slot stores 1)
   __syncthreads();
+  TAB_STAMP(4);
   uint32_t mark = 0, gpre = 0;
   if (tid < 256) {
     mark = s_group[tid];
@@ -107,6 +126,7 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     if (lane == 0) s_gcnt[wave] = (uint32_t)__popcll(m);
   }
   __syncthreads();
+  TAB_STAMP(5);
   if (tid < 256) {
     uint32_t g = gpre;
     for (uint32_t w = 0; w < wave; ++w) g += s_gcnt[w];
@@ -114,18 +134,30 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     if (tid == 255) s_ngroups = g + mark;
   }
   __syncthreads();
+  TAB_STAMP(6);
+  // only the used subtables (dummy + one per group) are ever read: zero just those
+  const uint32_t used_vec = (s_ngroups + 1u) * 32u;
+  for (uint32_t i = tid; i < used_vec; i += blockDim.x) s_t2v[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  TAB_STAMP(7);
   if (!bad && tid < 256 && L) {
-    const uint16_t e = (uint16_t)(tid | (L << 8));
-    if (L <= 8) {
-      for (uint32_t i = 0; i < (1u << (8 - L)); ++i) s_t1[(code >> 8) + i] = e;
+    // a code's range is aligned to its size: ranges of >= 8 entries go out as
+    // 16-byte LDS stores (a 9-bit code: 16 stores, not 128)
+    const uint32_t e = tid | (L << 8);
+    uint16_t *dst = L <= 8 ? s_t1 + (code >> 8) : s_t2 + s_group[code >> 8] * 256u + (code & 0xFFu);
+    const uint32_t n = L <= 8 ? 1u << (8 - L) : 1u << (16 - L);
+    if (n >= 8) {
+      const uint32_t e2 = e | (e << 16);
+      uint4 *v = reinterpret_cast<uint4 *>(dst);
+      for (uint32_t i = 0; i < n / 8; ++i) v[i] = make_uint4(e2, e2, e2, e2);
     } else {
-      uint16_t *sub = s_t2 + s_group[code >> 8] * 256u + (code & 0xFFu);
-      for (uint32_t i = 0; i < (1u << (16 - L)); ++i) sub[i] = e;
+      for (uint32_t i = 0; i < n; ++i) dst[i] = (uint16_t)e;
     }
   }
   __syncthreads();  // (valid prefix code: a group's high byte carries no short code)
   if (tid < 256 && s_group[tid]) s_t1[tid] = (uint16_t)s_group[tid];
   __syncthreads();
+  TAB_STAMP(8);
   if (blockIdx.x == 0) {
     // out: T1, T2 over its whole capacity (zero past the used subtables)
     if (((uintptr_t)t1 & 15u) == 0) {
@@ -135,9 +167,9 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     }
     if (((uintptr_t)t2 & 15u) == 0) {
       uint4 *v = reinterpret_cast<uint4 *>(t2);
-      for (uint32_t i = tid; i < kT2Vec; i += blockDim.x) v[i] = s_t2v[i];
+      for (uint32_t i = tid; i < kT2Vec; i += blockDim.x) v[i] = i < used_vec ? s_t2v[i] : make_uint4(0, 0, 0, 0);
     } else {
-      for (uint32_t i = tid; i < (uint32_t)MH_TABLE2_MAX_ENTRIES; i += blockDim.x) t2[i] = s_t2[i];
+      for (uint32_t i = tid; i < (uint32_t)MH_TABLE2_MAX_ENTRIES; i += blockDim.x) t2[i] = i < used_vec * 8 ? s_t2[i] : 0;
     }
     if (tid == 0) {
       *t2_entries = bad ? 256u : (s_ngroups + 1u) * 256u;
@@ -187,6 +219,8 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
       out14[q] = (uint16_t)((e >> 8) <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
     }
   }
+  __syncthreads();
+  TAB_STAMP(15);
 }
 
 }  // namespace
