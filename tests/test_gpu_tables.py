@@ -76,3 +76,34 @@ def test_device_tables_reject_bad_headers(mh, device, bad, status):
         dev.check_status()
     assert ei.value.status == status
     assert not dev.table1.cpu().numpy().any()
+
+
+def test_device_tables_random_headers(mh, device):
+    """40 canonical headers from random histograms (short and long codes, a few
+    symbols to all 256, lengths up to 16): T1, T2 and the prepared table built on the
+    device equal the host builder + mh_prepare_lut byte for byte (the device derives
+    P0 and the longest/shortest-code words from the canonical codes)."""
+    import ctypes
+    import torch
+    from metalhuffman_amd import _native as N
+    from metalhuffman_amd import decoder as D
+    rng = np.random.default_rng(77)
+    done = 0
+    while done < 40:
+        k = int(rng.integers(2, 257))
+        f = np.zeros(256, np.uint64)
+        syms = rng.choice(256, k, replace=False)
+        f[syms] = np.round(2.0 ** rng.uniform(0, rng.uniform(2, 17), k)).astype(np.uint64)
+        canon = np.zeros(256, np.uint8)
+        if N.lib().mh_code_lengths(f.ctypes.data_as(N._u64p), canon.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))):
+            continue  # depth > 16: not a valid header
+        t1, t2 = mh.Huffman.generateSplitLookupTables(canon)
+        dev = D.DeviceTables.from_canonical_header(canon, device)
+        assert dev.check_status() * 2 == t2.size
+        assert np.array_equal(dev.table1.cpu().numpy(), t1)
+        d2 = dev.table2.cpu().numpy()
+        assert np.array_equal(d2[: t2.size], t2) and not d2[t2.size:].any()
+        host = D.DeviceTables.upload(t1, t2, device)
+        torch.cuda.synchronize(device)
+        assert np.array_equal(dev.lut.cpu().numpy(), host.lut.cpu().numpy()), (k, int(canon.max()))
+        done += 1
