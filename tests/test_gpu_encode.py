@@ -180,3 +180,26 @@ def test_async_encode_many_frames_back_to_back(mh, device, bigbridge):
             assert np.array_equal(r.canon, ref.canon)
             assert np.array_equal(r.codes.cpu().numpy(), ref.codes)
             assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)
+
+
+def test_async_encode_fuzz_shapes_and_histograms(mh, device):
+    """Random sizes (partial blocks included) and random delta histograms, from a
+    few symbols to all 256 and codes up to 16 bits: the device tree, codes and
+    offsets equal the host codec's, and the device-only decode returns the frame."""
+    rng = np.random.default_rng(2024)
+    done = 0
+    while done < 16:
+        h, w = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        k = int(rng.integers(1, 257))
+        syms = rng.choice(256, k, replace=False)
+        p = 2.0 ** rng.uniform(0, rng.uniform(1, 14), k)
+        nb = ((w + 7) // 8) * ((h + 7) // 8)
+        d = rng.choice(syms, size=nb * 64, p=p / p.sum()).astype(np.uint8)
+        bw = (w + 7) // 8
+        img = image_from_block_deltas(d, bw * 8, nb // bw * 8)[:h, :w]
+        try:
+            mh.encode_frame(img)
+        except mh.MHError:
+            continue  # depth > 16 after the crop's zero padding: not a valid frame
+        _check_async(mh, device, np.ascontiguousarray(img))
+        done += 1
