@@ -6,7 +6,10 @@ of mdejong/MetalHuffman).
   * csrc/mh_host.cpp                host producer: encoder, canonical codes, T1/T2
   * codec.Huffman                   the reference's `Huffman` facade (Shared/Huffman.h)
   * decoder.decode / DeviceFrames   GPU decode of one frame or a batch
-  * dist                            frame sharding + table broadcast (RCCL / gloo)
+  * decoder.DeviceTables            T1/T2 + prepared table (uploaded, or built on the device)
+  * encoder.Encoder                 GPU encoder (encode / encode_async: no host sync)
+  * stream                          streaming from host memory (config 5)
+  * dist                            frame sharding, single-frame bands, table broadcast
 """
 from ._native import EXPORTS, LIB_PATH, MH_CODES_PAD, MH_FLAG_NO_DELTA, MHError, lib
 from .codec import BLOCK_DIM, EncodedFrame, Huffman, block_grid, encode_frame, merge_blocks, split_blocks
