@@ -325,12 +325,20 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   if (lane == 0) atomicAdd(&s_total, (unsigned long long)bits);
   __syncthreads();
   MH_TREE_STAMP(6);
-  if (tid == 0) {
-    uint32_t code = 0;  // first code of each length: shift left across every length step
-    for (uint32_t l = 1; l <= 16; ++l) {
-      s_first[l] = code;
-      code = (code + s_wcnt[0][l] + s_wcnt[1][l] + s_wcnt[2][l] + s_wcnt[3][l]) << 1;
+  if (tid < 64) {
+    // first code of each length, the recurrence code = (code + count) << 1 in closed
+    // form: first[l] = sum over j < l of count[j] << (l - j), a 16-lane prefix sum of
+    // count[j] << (16 - j) (<= 2^23) shifted back down
+    const uint32_t ln = (tid & 15u) + 1u;
+    const uint32_t cnt = tid < 16 ? s_wcnt[0][ln] + s_wcnt[1][ln] + s_wcnt[2][ln] + s_wcnt[3][ln] : 0u;
+    const uint32_t v = cnt << (16 - ln);
+    uint32_t incl = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if ((tid & 63u) >= d) incl += y;
     }
+    if (tid < 16) s_first[ln] = (incl - v) >> (16 - ln);
   }
   __syncthreads();
   MH_TREE_STAMP(7);

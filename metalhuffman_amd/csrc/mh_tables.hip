@@ -81,14 +81,21 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
   }
   __syncthreads();
   TAB_STAMP(2);
-  if (tid == 0) {
-    // first code of each length: shift left across every length step
-    uint32_t code = 0;
-    for (uint32_t l = 1; l <= 16; ++l) {
-      s_first[l] = code;
-      code = (code + s_wcnt[0][l] + s_wcnt[1][l] + s_wcnt[2][l] + s_wcnt[3][l]) << 1;
+  if (tid == 0 && s_kraft > 65536u) s_bad |= 2u;
+  if (tid < 64) {
+    // first code of each length, the recurrence code = (code + count) << 1 in closed
+    // form: first[l] = sum over j < l of count[j] << (l - j), a 16-lane prefix sum of
+    // count[j] << (16 - j) (<= 2^23) shifted back down
+    const uint32_t ln = (tid & 15u) + 1u;
+    const uint32_t cnt = tid < 16 ? s_wcnt[0][ln] + s_wcnt[1][ln] + s_wcnt[2][ln] + s_wcnt[3][ln] : 0u;
+    const uint32_t v = cnt << (16 - ln);
+    uint32_t incl = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if ((tid & 63u) >= d) incl += y;
     }
-    if (s_kraft > 65536u) s_bad |= 2u;
+    if (tid < 16) s_first[ln] = (incl - v) >> (16 - ln);
   }
   __syncthreads();
   TAB_STAMP(3);
