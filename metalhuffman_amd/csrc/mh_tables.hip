@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
   __shared__ __attribute__((aligned(16))) uint16_t s_t2[MH_TABLE2_MAX_ENTRIES];
   __shared__ __attribute__((aligned(16))) uint16_t s_t1[256];
   __shared__ uint32_t s_group[256], s_wcnt[4][17], s_gcnt[4];
-  __shared__ uint32_t s_first[17], s_kraft, s_bad, s_ngroups, s_mx, s_mn;
+  __shared__ uint32_t s_first[17], s_bad, s_ngroups, s_mx, s_mn;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
 #ifdef MH_TABLE_STAMPS
 #define TAB_STAMP(i) \
@@ -60,7 +60,6 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
     s_group[tid] = 0;
   }
   if (tid == 0) {
-    s_kraft = 0;
     s_bad = 0;
     s_mx = 0;
     s_mn = 255;
@@ -71,8 +70,8 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
   // one ballot per length per wave
   uint32_t in_wave = 0;
   if (tid < 256) {
-    if (L > 16) atomicOr(&s_bad, 1u);
-    else if (L) atomicAdd(&s_kraft, 1u << (16 - L));
+    // (no LDS atomics on one word here: 256 of them serialise, ~18 clocks each)
+    if (__ballot(L > 16) && lane == 0) s_bad = 1u;
     for (uint32_t l = 1; l <= 16; ++l) {
       const uint64_t m = __ballot(L == l);
       if (L == l) in_wave = (uint32_t)__popcll(m & below);
@@ -81,7 +80,6 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
   }
   __syncthreads();
   TAB_STAMP(2);
-  if (tid == 0 && s_kraft > 65536u) s_bad |= 2u;
   if (tid < 64) {
     // first code of each length, the recurrence code = (code + count) << 1 in closed
     // form: first[l] = sum over j < l of count[j] << (l - j), a 16-lane prefix sum of
@@ -96,6 +94,7 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
       if ((tid & 63u) >= d) incl += y;
     }
     if (tid < 16) s_first[ln] = (incl - v) >> (16 - ln);
+    if (tid == 15 && incl > 65536u) s_bad |= 2u;  // Kraft sum over 1: not a prefix code
   }
   __syncthreads();
   TAB_STAMP(3);
