@@ -61,9 +61,6 @@ __device__ __forceinline__ void split_lookup_batch(const uint16_t *s_t1, const u
     if ((e[k] >> 8) == 0) e[k] = idx[k] < t2_entries ? v[k] : 0u;
 }
 
-// mh_prepare_lut: the 13-bit two-level table (as build_lut) and the 14-bit single
-// table (as build_lut14) from T1/T2, one workgroup. T1 is staged in LDS and the T2
-// reads go out in batches of 8 independent loads (15.6 -> see DESIGN.md).
 // The prepared buffer from T1 (in LDS) and T2 (LDS or global, t2_entries long;
 // reads past it are the all-zero entry), by the whole workgroup:
 //   L1[p] (p = 13-bit prefix): step_word of the window p << 3 when its code has
@@ -114,9 +111,17 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     }
   }
   for (uint32_t i = tid; i < (uint32_t)(kLutEntries - kL1Entries); i += nt) lut[kL1Entries + i] = 0;
-  atomicMin(&p0, my_p0);
-  atomicMax(&mx, my_mx);
-  atomicMin(&mn, my_mn);
+  // wave reductions first: a thousand LDS atomics on one word serialise
+  for (uint32_t o = 32; o; o >>= 1) {
+    my_p0 = min(my_p0, (uint32_t)__shfl_xor(my_p0, o));
+    my_mx = max(my_mx, (uint32_t)__shfl_xor(my_mx, o));
+    my_mn = min(my_mn, (uint32_t)__shfl_xor(my_mn, o));
+  }
+  if ((tid & 63u) == 0) {
+    atomicMin(&p0, my_p0);
+    atomicMax(&mx, my_mx);
+    atomicMin(&mn, my_mn);
+  }
   __syncthreads();
   // escapes and the second level (the long codes), as build_lut
   const uint32_t P0 = p0;
@@ -134,6 +139,5 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
   if (tid < 4)
     reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[tid] = tid == 0 ? mx : tid == 1 ? mn : 0u;
 }
-
 
 }  // namespace
