@@ -20,3 +20,15 @@ for spec in frame:200:20 batch:256:256 tile8192:512:512 tile8192_random:512:512;
   { echo "== bench.py --workload $wl --steps $k --warmup $w (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl $k; } >> gpurun_out/ktrace_summary.txt
 done
 cat gpurun_out/ktrace_summary.txt
+# producer side: the GPU encoder (async, back to back) and the device-only chain
+rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_encode
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_encode -o run -- python3 scripts/enc_profile.py 64 > gpurun_out/enc_profile.log 2>&1 || { tail gpurun_out/enc_profile.log; exit 1; }
+timeout -k 10 60 ./host/mh_decode_host device 2048 1536 200 > gpurun_out/device_chain.log 2>&1 || { cat gpurun_out/device_chain.log; exit 1; }
+python3 - > gpurun_out/encoder_ktrace.txt <<'PY'
+import csv
+print(open("gpurun_out/enc_profile.log").read().strip().splitlines()[-1])
+print(open("gpurun_out/device_chain.log").read().strip())
+for r in sorted(csv.DictReader(open("gpurun_out/prof_encode/run_kernel_stats.csv")), key=lambda r: -float(r["AverageNs"])):
+    print(f"{float(r['AverageNs']) / 1e3:8.2f} us  x{r['Calls']:>4}  {r['Name'][:80]}")
+PY
+cat gpurun_out/encoder_ktrace.txt
