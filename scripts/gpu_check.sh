@@ -26,7 +26,7 @@ timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 timeout -k 10 60 ./host/mh_decode_host device 2048 1536 200 > gpurun_out/device_chain.log 2>&1 || { cat gpurun_out/device_chain.log; exit 1; }
 python3 - > gpurun_out/encoder_ktrace.txt <<'PY'
 import csv
-print(open("gpurun_out/enc_profile.log").read().strip().splitlines()[-1])
+print([l for l in open("gpurun_out/enc_profile.log") if "async encode" in l][-1].strip())
 print(open("gpurun_out/device_chain.log").read().strip())
 for r in sorted(csv.DictReader(open("gpurun_out/prof_encode/run_kernel_stats.csv")), key=lambda r: -float(r["AverageNs"])):
     print(f"{float(r['AverageNs']) / 1e3:8.2f} us  x{r['Calls']:>4}  {r['Name'][:80]}")
