@@ -49,3 +49,20 @@ def test_band_bounds():
         ef.band(0, 9)
     b = ef.band(7, 8)           # last block row
     assert b.height == 8 and b.block_offsets[0] == ef.block_offsets[56] % 8
+
+
+def test_more_ranks_than_block_rows():
+    import metalhuffman_amd as mh
+    from metalhuffman_amd import dist as MD
+    from metalhuffman_amd import frames as F
+    from oracle import oracle as O
+    img = np.ascontiguousarray(F.bigbridge()[:20, :40])   # 3 block rows
+    ef = mh.encode_frame(img)
+    t1, t2 = ef.tables()
+    got = []
+    for r in range(5):
+        band, y0 = MD.frame_band(ef, 5, r)
+        if band is None:
+            continue
+        got.append(O.decode_frame_shader(band.block_offsets, band.codes, t1, t2, band.width, band.height))
+    assert len(got) == 3 and np.array_equal(np.concatenate(got), img)
