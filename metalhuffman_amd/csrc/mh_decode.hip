@@ -24,6 +24,8 @@
 
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/metalhuffman.h"
 #include "mh_lut.hpp"
 
@@ -816,39 +818,62 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 #endif
 }
 
-int g_cu_count = 0;
-int g_occ[2][kMaxWavesPerWG + 1];
-
-int cu_count() {
-  if (!g_cu_count) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-    g_cu_count = prop.multiProcessorCount;
-  }
-  return g_cu_count;
-}
+// Per-device launch parameters (CU count, batch-kernel occupancy per workgroup
+// size), computed once per device ordinal under std::call_once: no mutable state
+// is shared between devices or written by concurrent callers (the reference keeps
+// its tables in module statics, Shared/HuffmanUtil.cpp:87-102).
+constexpr int kMaxDevices = 64;
+struct DeviceInfo {
+  std::once_flag once;
+  int cus = 0;
+  int occ[2][kMaxWavesPerWG + 1] = {};
+};
+DeviceInfo g_devinfo[kMaxDevices];
 
 template <bool kDelta>
-int occupancy(int nw) {
-  int &o = g_occ[kDelta ? 1 : 0][nw];
-  if (!o) {
-    int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_decode_kernel<kDelta>, nw * 64, 0) !=
-            hipSuccess ||
-        blocks < 1)
-      blocks = 1;
-    o = blocks;
-  }
-  return o;
+int occupancy_query(int nw) {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_decode_kernel<kDelta>, nw * 64, 0) !=
+          hipSuccess ||
+      blocks < 1)
+    blocks = 1;
+  return blocks;
+}
+
+// The device a launch on `s` runs on (the stream's, or the caller's current one).
+int stream_device(hipStream_t s) {
+  int dev = -1;
+  if (s && hipStreamGetDevice(s, &dev) == hipSuccess) return dev;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  return dev;
+}
+
+const DeviceInfo *device_info(hipStream_t s) {
+  const int dev = stream_device(s);
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  DeviceInfo &d = g_devinfo[dev];
+  std::call_once(d.once, [&] {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    int cur = -1;
+    const bool swap = hipGetDevice(&cur) == hipSuccess && cur != dev;
+    if (swap && hipSetDevice(dev) != hipSuccess) return;
+    for (int nw = 1; nw <= kMaxWavesPerWG; ++nw) {
+      d.occ[0][nw] = occupancy_query<false>(nw);
+      d.occ[1][nw] = occupancy_query<true>(nw);
+    }
+    if (swap) (void)hipSetDevice(cur);
+    d.cus = prop.multiProcessorCount;  // last: nonzero marks the entry complete
+  });
+  return d.cus ? &d : nullptr;
 }
 
 template <bool kDelta>
 int launch(const DecodeArgs &a0, hipStream_t s) {
   DecodeArgs a = a0;
-  const int cus = cu_count();
-  if (!cus) return MH_ERR_HIP;
+  const DeviceInfo *di = device_info(s);
+  if (!di) return MH_ERR_HIP;
+  const int cus = di->cus;
   if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // one tile per wave, kSmallWaves waves per workgroup: fewer workgroups copy the
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
@@ -863,7 +888,7 @@ int launch(const DecodeArgs &a0, hipStream_t s) {
   if (nw < 1) nw = 1;
   if (nw > (uint32_t)kMaxWavesPerWG) nw = kMaxWavesPerWG;
   a.n_groups = (a.total_tiles + nw - 1) / nw;
-  const uint32_t resident = (uint32_t)(cus * occupancy<kDelta>((int)nw));
+  const uint32_t resident = (uint32_t)(cus * di->occ[kDelta ? 1 : 0][nw]);
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
   hipLaunchKernelGGL(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), 0, s, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;

@@ -389,30 +389,76 @@ typedef struct {
   const uint8_t *const *bufs;
   uint8_t *const *outs;
   uint32_t n_frames, n_threads, tid, reps;
+  uint32_t w, h;      /* pipeline mode: raster size (0: symbols only) */
+  uint8_t *scratch;   /* pipeline mode: nsym block-order symbols per thread */
 } orc_job;
+
+/* Block-order deltas -> W x H raster: the per-block prefix sum
+ * (HuffmanUtil::decodeSignedByteDeltas, HuffmanUtil.cpp:49-78, per 64-symbol block as
+ * the renderer's producer step delta-encodes per block, AAPLRenderer.m:374-688) and the
+ * block merge (Util.m:233-323's inverse: block (bx, by) row r -> raster row 8 by + r). */
+static void undelta_raster(uint8_t *sym, uint32_t w, uint32_t h, uint8_t *raster) {
+  const uint32_t bw = (w + 7) / 8, bh = (h + 7) / 8;
+  for (uint32_t b = 0; b < bw * bh; b++) orc_delta_decode(sym + (size_t)b * 64, 64);
+  for (uint32_t y = 0; y < h; y++) {
+    const uint32_t by = y / 8, ry = y % 8;
+    for (uint32_t bx = 0; bx < bw; bx++) {
+      const uint32_t x0 = bx * 8, n = x0 + 8 <= w ? 8 : w - x0;
+      memcpy(raster + (size_t)y * w + x0, sym + ((size_t)(by * bw + bx) * 64 + ry * 8), n);
+    }
+  }
+}
 
 static void *decode_worker(void *arg) {
   orc_job *j = (orc_job *)arg;
   for (uint32_t r = 0; r < j->reps; r++)
-    for (uint32_t f = j->tid; f < j->n_frames; f += j->n_threads)
-      orc_decode_from_tables(j->t1, j->t2, j->nsym, j->bufs[f], j->outs[f], NULL);
+    for (uint32_t f = j->tid; f < j->n_frames; f += j->n_threads) {
+      if (j->w) {
+        orc_decode_from_tables(j->t1, j->t2, j->nsym, j->bufs[f], j->scratch, NULL);
+        undelta_raster(j->scratch, j->w, j->h, j->outs[f]);
+      } else {
+        orc_decode_from_tables(j->t1, j->t2, j->nsym, j->bufs[f], j->outs[f], NULL);
+      }
+    }
   return NULL;
+}
+
+static double time_jobs(const orc_sym *t1, const orc_sym *t2, uint32_t nsym,
+                        const uint8_t *const *bufs, uint8_t *const *outs, uint32_t n_frames,
+                        uint32_t n_threads, uint32_t reps, uint32_t w, uint32_t h) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 1024) n_threads = 1024;
+  pthread_t *th = (pthread_t *)calloc(n_threads, sizeof(pthread_t));
+  orc_job *jobs = (orc_job *)calloc(n_threads, sizeof(orc_job));
+  if (!th || !jobs) {
+    free(th);
+    free(jobs);
+    return -1.0;
+  }
+  for (uint32_t t = 0; t < n_threads; t++) {
+    jobs[t] = (orc_job){t1, t2, nsym, bufs, outs, n_frames, n_threads, t, reps, w, h, NULL};
+    if (w) jobs[t].scratch = (uint8_t *)malloc(nsym);
+  }
+  struct timespec t0, t1c;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (uint32_t t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, decode_worker, &jobs[t]);
+  for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1c);
+  for (uint32_t t = 0; t < n_threads; t++) free(jobs[t].scratch);
+  free(th);
+  free(jobs);
+  return (double)(t1c.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1c.tv_nsec - t0.tv_nsec);
 }
 
 double orc_time_decode_frames(const orc_sym *t1, const orc_sym *t2, uint32_t nsym,
                               const uint8_t *const *bufs, uint8_t *const *outs,
                               uint32_t n_frames, uint32_t n_threads, uint32_t reps) {
-  if (n_threads < 1) n_threads = 1;
-  if (n_threads > 256) n_threads = 256;
-  pthread_t th[256];
-  orc_job jobs[256];
-  struct timespec t0, t1c;
-  clock_gettime(CLOCK_MONOTONIC, &t0);
-  for (uint32_t t = 0; t < n_threads; t++) {
-    jobs[t] = (orc_job){t1, t2, nsym, bufs, outs, n_frames, n_threads, t, reps};
-    pthread_create(&th[t], NULL, decode_worker, &jobs[t]);
-  }
-  for (uint32_t t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
-  clock_gettime(CLOCK_MONOTONIC, &t1c);
-  return (double)(t1c.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1c.tv_nsec - t0.tv_nsec);
+  return time_jobs(t1, t2, nsym, bufs, outs, n_frames, n_threads, reps, 0, 0);
+}
+
+double orc_time_decode_pipeline(const orc_sym *t1, const orc_sym *t2, uint32_t w, uint32_t h,
+                                const uint8_t *const *bufs, uint8_t *const *rasters,
+                                uint32_t n_frames, uint32_t n_threads, uint32_t reps) {
+  const uint32_t nsym = ((w + 7) / 8) * ((h + 7) / 8) * 64;
+  return time_jobs(t1, t2, nsym, bufs, rasters, n_frames, n_threads, reps, w, h);
 }

@@ -102,6 +102,13 @@ double orc_time_decode_frames(const orc_sym *t1, const orc_sym *t2, uint32_t nsy
                               const uint8_t *const *bufs, uint8_t *const *outs,
                               uint32_t n_frames, uint32_t n_threads, uint32_t reps);
 
+/* CPU baseline, full pipeline: as orc_time_decode_frames, then each frame's
+ * block-order deltas are integrated per block and merged into its W x H raster
+ * (decode + undelta + raster, what a CPU consumer of the reference's buffers does). */
+double orc_time_decode_pipeline(const orc_sym *t1, const orc_sym *t2, uint32_t w, uint32_t h,
+                                const uint8_t *const *bufs, uint8_t *const *rasters,
+                                uint32_t n_frames, uint32_t n_threads, uint32_t reps);
+
 #ifdef __cplusplus
 }
 #endif

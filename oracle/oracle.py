@@ -67,6 +67,10 @@ def lib():
                                              ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_time_decode_frames.restype = ctypes.c_double
+        L.orc_time_decode_pipeline.argtypes = [_u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.POINTER(_u8p), ctypes.POINTER(_u8p),
+                                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_time_decode_pipeline.restype = ctypes.c_double
         L.orc_check_frame.argtypes = [_u32p, _u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_uint32,
                                       ctypes.c_uint32, _u32p]
         _lib = L
@@ -216,6 +220,18 @@ def time_decode_frames(t1, t2, nsym: int, bufs: list, n_threads: int, reps: int 
     b_arr = BA(*[_p(b) for b in bufs])
     o_arr = BA(*[_p(o) for o in outs])
     return lib().orc_time_decode_frames(_p(t1), _p(t2), nsym, b_arr, o_arr, n, n_threads, reps)
+
+
+def time_decode_pipeline(t1, t2, w: int, h: int, bufs: list, n_threads: int, reps: int = 1,
+                         rasters: list | None = None) -> float:
+    """Wall seconds to decode + undelta + raster `bufs` (frame-parallel on n_threads),
+    repeated `reps` times. `rasters` (optional) receives the last pass's W x H frames."""
+    n = len(bufs)
+    outs = rasters if rasters is not None else [np.zeros((h, w), np.uint8) for _ in range(n)]
+    BA = _u8p * n
+    b_arr = BA(*[_p(b) for b in bufs])
+    o_arr = BA(*[_p(o) for o in outs])
+    return lib().orc_time_decode_pipeline(_p(t1), _p(t2), w, h, b_arr, o_arr, n, n_threads, reps)
 
 
 def ref_encode(sym: np.ndarray, stride: int = 64, with_header: bool = False):

@@ -354,3 +354,28 @@ def test_single_frame_bands(mh, device, bigbridge, world):
             assert np.array_equal(out, img[y0: y0 + band.height]), (img.shape, world, r)
             rows.append(out)
         assert np.array_equal(np.concatenate(rows), img)
+
+
+def test_config4_full_shard_one_launch(mh, oracle, device, bigbridge):
+    """BASELINE config 4 at its per-GPU size: a 64-frame block-shuffled shard (512
+    frames / 8 GPUs) decoded in ONE launch of the batch kernel. Every frame equals its
+    input; two frames also equal the oracle's shader-semantics decode (the DEBUG
+    self-check of Shared/AAPLRenderer.m:616-650, here against the restatement)."""
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import frames as F
+    imgs = [F.block_shuffle(bigbridge, 5000 + s) for s in range(64)]
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(8) as ex:  # ctypes releases the GIL
+        efs = list(ex.map(mh.encode_frame, imgs))
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    fr = D.DeviceFrames.pack(efs, device)
+    assert fr.n_frames == 64
+    out = D.decode(fr, tabs)
+    ref = torch.from_numpy(np.stack(imgs)).to(device)
+    torch.cuda.synchronize(device)
+    bad = [i for i in range(64) if not torch.equal(out[i, :, :2048], ref[i])]
+    assert not bad, bad
+    for i in (0, 41):
+        assert np.array_equal(out[i, :, :2048].cpu().numpy(), _oracle_decode(oracle, efs[i])), i

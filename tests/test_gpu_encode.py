@@ -203,3 +203,32 @@ def test_async_encode_fuzz_shapes_and_histograms(mh, device):
             continue  # depth > 16 after the crop's zero padding: not a valid frame
         _check_async(mh, device, np.ascontiguousarray(img))
         done += 1
+
+
+@pytest.mark.parametrize("wl", ["bigbridge", "bigbridge_crop_777x1001", "random_1024_seed1234",
+                                "bigbridge_shuffle_seed7", "tile_8192"])
+def test_device_encoder_matches_reference_encoder_hashes(mh, device, bigbridge, wl):
+    """The device encoder pinned DIRECTLY to the reference encoder: SHA-256 of its
+    canonical header, huffBuff (codes + zero pad) and block offsets equal those of
+    Shared/HuffmanEncoder.cpp:310-381 compiled here (tests/golden/golden.json), not
+    only the host codec's bytes."""
+    import hashlib
+    import torch
+    from helpers import golden
+    from metalhuffman_amd import frames as F
+    from metalhuffman_amd.encoder import encode_frame_device
+    rec = golden()["workloads"][wl]
+    img = {"bigbridge": lambda: bigbridge,
+           "bigbridge_crop_777x1001": lambda: F.crop(bigbridge, 1001, 777),
+           "random_1024_seed1234": lambda: F.uniform_random(1024, 1024, 1234),
+           "bigbridge_shuffle_seed7": lambda: F.block_shuffle(bigbridge, 7),
+           "tile_8192": lambda: F.mirror_tile(bigbridge, 8192, 8192)}[wl]()
+    sha = lambda b: hashlib.sha256(np.ascontiguousarray(b).tobytes()).hexdigest()
+    assert sha(img) == rec["input_sha256"]
+    dev = encode_frame_device(torch.from_numpy(np.ascontiguousarray(img)).to(device))
+    torch.cuda.synchronize(device)
+    assert sha(dev.canon) == rec["canon_sha256"]
+    codes = dev.codes.cpu().numpy()
+    assert codes.size == rec["huffbuff_bytes"]
+    assert sha(codes) == rec["huffbuff_sha256"]
+    assert sha(dev.block_offsets.cpu().numpy().view(np.uint32).astype("<u4")) == rec["offsets_sha256"]

@@ -107,3 +107,17 @@ def test_device_tables_random_headers(mh, device):
         torch.cuda.synchronize(device)
         assert np.array_equal(dev.lut.cpu().numpy(), host.lut.cpu().numpy()), (k, int(canon.max()))
         done += 1
+
+
+def test_device_tables_bigbridge_golden_hashes(mh, device, bigbridge):
+    """Device-built T1/T2 for BigBridge pinned to the recorded SHA-256 (SURVEY.md 8(c),
+    golden.json), not only to the host builder."""
+    import hashlib
+    from metalhuffman_amd import decoder as D
+    rec = golden()["workloads"]["bigbridge"]
+    dev = D.DeviceTables.from_canonical_header(mh.encode_frame(bigbridge).canon, device)
+    entries = dev.check_status()
+    assert entries * 2 == rec["t2_bytes"]
+    sha = lambda b: hashlib.sha256(np.ascontiguousarray(b).tobytes()).hexdigest()
+    assert sha(dev.table1.cpu().numpy()) == rec["t1_sha256"]
+    assert sha(dev.table2.cpu().numpy()[: rec["t2_bytes"]]) == rec["t2_sha256"]

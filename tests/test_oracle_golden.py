@@ -80,7 +80,8 @@ def test_kat_6x4_not_square(oracle):
 
 
 @pytest.mark.parametrize("wl", ["bigbridge", "bigbridge_crop_777x1001", "random_1024_seed1234",
-                                "bigbridge_shuffle_seed7", "image_png_L_256", "image_png_L_512"])
+                                "bigbridge_shuffle_seed7", "image_png_L_256", "image_png_L_512",
+                                "tile_8192"])
 def test_workload_hashes(oracle, bigbridge, wl):
     from metalhuffman_amd import frames as F
     rec = golden()["workloads"][wl]
@@ -92,6 +93,8 @@ def test_workload_hashes(oracle, bigbridge, wl):
         img = F.uniform_random(1024, 1024, 1234)
     elif wl == "bigbridge_shuffle_seed7":
         img = F.block_shuffle(bigbridge, 7)
+    elif wl == "tile_8192":
+        img = F.mirror_tile(bigbridge, 8192, 8192)
     else:
         from PIL import Image
         gray = np.array(Image.open(os.path.join(GOLDEN, "Image.png")).convert("L"), np.uint8)
@@ -158,3 +161,20 @@ def test_block_deltas_helper_roundtrip(oracle):
     for b in range(blocks.size // 64):
         blocks[b * 64:(b + 1) * 64] = oracle.delta_encode(blocks[b * 64:(b + 1) * 64])
     assert np.array_equal(blocks, d)
+
+
+def test_cpu_baseline_pipeline_rasters(oracle, mh):
+    """bench.py's CPU pipeline leg (decode + undelta + raster) reproduces the frames
+    it times, on 3 threads over 5 frames of a partial-block crop."""
+    from metalhuffman_amd import frames as F
+    base = np.ascontiguousarray(F.bigbridge()[:203, :517])
+    imgs = [base] + [np.ascontiguousarray(np.roll(base, 37 * k, axis=1)) for k in range(1, 5)]
+    pairs = [(mh.encode_frame(im), im) for im in imgs]
+    pairs = [p for p in pairs if np.array_equal(p[0].canon, pairs[0][0].canon)]
+    efs, imgs = [p[0] for p in pairs], [p[1] for p in pairs]
+    t1, t2 = efs[0].tables()
+    ras = [np.zeros((203, 517), np.uint8) for _ in efs]
+    sec = oracle.time_decode_pipeline(t1, t2, 517, 203, [ef.codes for ef in efs], 3, reps=2, rasters=ras)
+    assert sec > 0
+    for r, im in zip(ras, imgs):
+        assert np.array_equal(r, im)
