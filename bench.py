@@ -113,7 +113,7 @@ class Workload:
                 n += 1
         return n
 
-    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=25.0):
+    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=50.0):
         """Timed region: `steps` launches (one hipGraph replay, or eager), bracketed by
         barrier + synchronize; wall = max over ranks.
         Kernel durations: the same `steps` launches issued eagerly right after, each
@@ -143,6 +143,31 @@ class Workload:
             except Exception as e:  # pragma: no cover - fall back to eager launches
                 print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
                 graph = None
+        # the process's first timing-event records initialise HIP's event timing
+        # (measured +40 us on the first timed region): do that off the clock
+        for _ in range(2):
+            wa, wb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            wa.record()
+            if graph is not None:
+                graph.replay()
+            wb.record()
+            torch.cuda.synchronize(dev)
+            wa.elapsed_time(wb)
+        diag = int(os.environ.get("MH_BENCH_DIAG_REPEAT", "0"))  # diagnostics: spread of the timed region
+        for k in range(diag):
+            if graph is not None and settle_ms:
+                t_end = time.perf_counter() + settle_ms * 1e-3
+                while time.perf_counter() < t_end:
+                    graph.replay()
+                    torch.cuda.synchronize(dev)
+            wa, wb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            ta = time.perf_counter()
+            wa.record()
+            graph.replay() if graph is not None else [self.launch(i) for i in range(steps)]
+            wb.record()
+            torch.cuda.synchronize(dev)
+            print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
         r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if world > 1:
             dist.barrier()
@@ -451,13 +476,22 @@ def main(argv=None) -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a HIP device")
     # MH_BENCH_BACKEND=gloo rehearses the multi-rank path on a one-GPU box (every
     # rank on the same device, CPU collectives); the driver's runs use RCCL
     backend = os.environ.get("MH_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
+    if os.environ.get("MH_BENCH_SYNC", "spin") == "spin":
+        # host waits spin (hipDeviceScheduleSpin) instead of yielding: the timed
+        # region's closing synchronize wakes without a scheduler round trip
+        # (single-shot 20-step walls: 138-147 us spin vs 141-177 us auto on one box,
+        # scripts/diag_timed_spread.sh). Set on this rank's device before its context.
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        if hip.hipSetDevice(ctypes.c_int(local)) == 0:
+            hip.hipSetDeviceFlags(ctypes.c_uint(1))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
