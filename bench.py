@@ -242,50 +242,71 @@ def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
     return r
 
 
-def stream_h2d(efs, tables, device, n_frames=2048, warmup=1024):
-    """BASELINE config 5 on one GPU through the native stream (mh_stream_*):
-    frames start in pinned host memory; each is copied H2D (codes + block offsets,
-    one hipMemcpyAsync) into one of two device slots and decoded by that slot's
-    captured graph, both on the slot's own stream, so the copy of frame i+1 (the
-    other slot) overlaps the decode of frame i. Reports sustained frames/s and decoded
-    MB/s including PCIe, and the single-frame latency (submit -> decoded, nothing
-    queued). Never the headline `value` (inputs are not resident in HBM)."""
-    from metalhuffman_amd.stream import FrameStream, pinned_frame
+def stream_h2d(efs, tables, device, n_frames=2048, n_cold=1000, n_paced=1000):
+    """BASELINE config 5 on this rank's GPU through the native stream group
+    (mh_stream_group_*, one member here; N members round-robin frames over N GPUs):
+    frames start in pinned host memory; each is copied H2D (codes + block offsets, one
+    DMA) into one of two device slots and decoded by that slot's captured graph, both
+    on the slot's own stream, so the copy of frame i+1 overlaps the decode of frame i.
+    Reports, on a freshly created stream (no warm-up excluded): the first n_cold
+    frames back to back and the very first frame's latency; then the sustained rate;
+    then n_paced frames one at a time (a 30 FPS consumer: nothing queued) with host
+    latency submit -> decoded (p50/p99/max) and device latency H2D start -> decode end.
+    Never the headline `value` (inputs are not resident in HBM)."""
+    from metalhuffman_amd.stream import FrameStreamGroup, pinned_frame
     W, H = efs[0].width, efs[0].height
     hosts = [pinned_frame(ef) for ef in efs]
-    fs = FrameStream(tables, W, H, max(ef.codes.size for ef in efs), slots=2, device=device)
+    cap = max(ef.codes.size for ef in efs)
+    g = FrameStreamGroup([tables], W, H, cap, slots=2)
+    c, o = hosts[0]
+    t = time.perf_counter()
+    m, sl = g.submit(c, o)
+    g.wait(m, sl)
+    first_us = (time.perf_counter() - t) * 1e6
 
-    def run(count):
+    def run(count, start=0):
         for i in range(count):
-            c, o = hosts[i % len(hosts)]
-            fs.submit(c, o)
-        fs.synchronize()
+            c, o = hosts[(start + i) % len(hosts)]
+            g.submit(c, o)
+        g.synchronize()
 
-    run(warmup)
+    t0 = time.perf_counter()
+    run(n_cold, 1)
+    cold_wall = time.perf_counter() - t0
     t0 = time.perf_counter()
     run(n_frames)
     wall = time.perf_counter() - t0
-    last = (n_frames - 1) % len(efs)
-    out_last = fs.output((warmup + n_frames - 1) % 2)[:, :W].clone()
-    lat = []
-    for i in range(64):  # one frame in flight at a time
+    host_lat, dev_lat = [], []
+    last = None
+    for i in range(n_paced):  # one frame in flight at a time
         c, o = hosts[i % len(hosts)]
         t = time.perf_counter()
-        fs.wait(fs.submit(c, o))
-        lat.append((time.perf_counter() - t) * 1e6)
-    fs.close()
+        m, sl = g.submit(c, o)
+        g.wait(m, sl)
+        host_lat.append((time.perf_counter() - t) * 1e6)
+        dev_lat.append(g.slot_time_ms(m, sl) * 1e3)
+        last = (i % len(hosts), m, sl)
+    out_last = g.output(last[1], last[2])[:, :W].clone()
+    g.close()
     from metalhuffman_amd import decoder as D
-    ref = D.decode(D.DeviceFrames.pack([efs[last]], device), tables)
+    ref = D.decode(D.DeviceFrames.pack([efs[last[0]]], device), tables)
     torch.cuda.synchronize(device)
     if not torch.equal(ref[0, :, :W], out_last):
         raise SystemExit("bench: streamed frame differs from the resident decode")
     h2d = float(np.mean([ef.codes.size + 4 * ef.n_blocks for ef in efs]))
-    lat.sort()
+    pct = lambda v, q: round(float(np.percentile(v, q)), 1)
     return {"frames": n_frames, "fps": round(n_frames / wall, 1),
             "value_MBps_incl_pcie": round(n_frames * W * H / wall / 1e6, 1),
             "h2d_bytes_per_frame": int(h2d), "h2d_GBps": round(n_frames * h2d / wall / 1e9, 2),
-            "latency_us_p50": round(lat[len(lat) // 2], 1), "latency_us_max": round(lat[-1], 1),
-            "slots": 2, "launch": "native mh_stream: per slot one stream, one H2D DMA + a captured hipGraph decode per frame"}
+            "cold_first_frames": n_cold + 1, "cold_fps": round(n_cold / cold_wall, 1),
+            "cold_first_frame_latency_us": round(first_us, 1),
+            "paced_frames": n_paced,
+            "latency_us_p50": pct(host_lat, 50), "latency_us_p99": pct(host_lat, 99),
+            "latency_us_max": round(max(host_lat), 1),
+            "device_latency_us_p50": pct(dev_lat, 50), "device_latency_us_p99": pct(dev_lat, 99),
+            "device_latency_us_max": round(max(dev_lat), 1),
+            "slots": 2, "members": g.size,
+            "launch": "native mh_stream_group: per slot one stream, one H2D DMA + a captured hipGraph decode per frame"}
 
 
 def copy_bandwidth(device, nbytes=1 << 30, reps=20):

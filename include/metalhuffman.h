@@ -204,8 +204,8 @@ typedef struct mh_stream mh_stream;
 /* A decode stream for frames shaped like `proto` (dims, flags, tables, d_lut;
  * a non-NULL proto->d_block_init means frames carry per-block init bytes; the
  * frame pointers in proto are ignored). It owns n_slots device slots of
- * codes_capacity code bytes each, a copy stream and a compute stream, and one
- * captured decode graph per slot. Slot i decodes into d_outputs[i] (caller
+ * codes_capacity code bytes each, one HIP stream per slot (its copies, then its
+ * decode), and one captured decode graph per slot. Slot i decodes into d_outputs[i] (caller
  * device buffers of round_up(W, 8) * H bytes, 8-byte aligned) or, when
  * d_outputs is NULL, into rasters the stream allocates. */
 int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_slots,
@@ -228,8 +228,29 @@ uint8_t *mh_stream_output(mh_stream *s, uint32_t slot, size_t *out_pitch);
 void *mh_stream_slot_stream(mh_stream *s, uint32_t slot);
 void *mh_stream_compute_stream(mh_stream *s);
 int mh_stream_wait(mh_stream *s, uint32_t slot);  /* that slot's decode done */
+/* Device-side latency of the slot's most recent frame (waits for it): from the
+ * start of its H2D copy to the end of its decode, in milliseconds. */
+int mh_stream_slot_time(mh_stream *s, uint32_t slot, float *ms);
+int mh_stream_device(mh_stream *s);               /* the HIP device it runs on */
 int mh_stream_synchronize(mh_stream *s);
 int mh_stream_destroy(mh_stream *s);
+
+/* Stream groups (config 5 on N GPUs of one node): n_members streams, member i on
+ * HIP device devices[i] with protos[i] (tables and d_lut resident on that device),
+ * n slots each; frames are round-robined over the members in submit order (frame
+ * k -> member k mod n). Every call sets the member's device for its duration and
+ * restores the caller's. A device may appear more than once. */
+typedef struct mh_stream_group mh_stream_group;
+int mh_stream_group_create(const mh_frame *protos, uint32_t n_members, const int *devices,
+                           uint64_t codes_capacity, uint32_t slots_per_member,
+                           mh_stream_group **out);
+int mh_stream_group_submit(mh_stream_group *g, const uint8_t *h_codes, uint64_t codes_bytes,
+                           const uint32_t *h_block_offsets, const uint8_t *h_block_init,
+                           uint32_t *member, uint32_t *slot);
+mh_stream *mh_stream_group_member(mh_stream_group *g, uint32_t member);
+uint32_t mh_stream_group_size(const mh_stream_group *g);
+int mh_stream_group_synchronize(mh_stream_group *g);
+int mh_stream_group_destroy(mh_stream_group *g);
 
 /* ---------------------------------------------------------------------- */
 /* Host-side producer (CPU, reentrant). Outputs are byte-identical to the   */

@@ -25,7 +25,9 @@ EXPORTS = (
     "mh_build_tables", "mh_build_single_table", "mh_error_string", "mh_device_count",
     "mh_build_tables_device", "mh_stream_create", "mh_stream_submit", "mh_stream_output",
     "mh_stream_compute_stream", "mh_stream_slot_stream", "mh_stream_wait", "mh_stream_synchronize",
-    "mh_stream_destroy",
+    "mh_stream_destroy", "mh_stream_slot_time", "mh_stream_device",
+    "mh_stream_group_create", "mh_stream_group_submit", "mh_stream_group_member", "mh_stream_group_size",
+    "mh_stream_group_synchronize", "mh_stream_group_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
     "mh_encode_frame_device_async",
     "mh_container_header", "mh_parse_container_header", "mh_check",
@@ -96,6 +98,18 @@ def lib() -> ctypes.CDLL:
         L.mh_stream_wait.argtypes = [_vp, ctypes.c_uint32]
         L.mh_stream_synchronize.argtypes = [_vp]
         L.mh_stream_destroy.argtypes = [_vp]
+        L.mh_stream_slot_time.argtypes = [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_float)]
+        L.mh_stream_device.argtypes = [_vp]
+        L.mh_stream_group_create.argtypes = [ctypes.POINTER(mh_frame), ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_int), ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.POINTER(_vp)]
+        L.mh_stream_group_submit.argtypes = [_vp, _vp, ctypes.c_uint64, _vp, _vp, _u32p, _u32p]
+        L.mh_stream_group_member.argtypes = [_vp, ctypes.c_uint32]
+        L.mh_stream_group_member.restype = _vp
+        L.mh_stream_group_size.argtypes = [_vp]
+        L.mh_stream_group_size.restype = ctypes.c_uint32
+        L.mh_stream_group_synchronize.argtypes = [_vp]
+        L.mh_stream_group_destroy.argtypes = [_vp]
         L.mh_code_lengths.argtypes = [_u64p, _u8p]
         L.mh_container_header.argtypes = [ctypes.c_uint64, _u8p]
         L.mh_parse_container_header.argtypes = [_u8p, _u64p]

@@ -31,7 +31,8 @@ struct mh_stream {
     uint8_t *init = nullptr;
     uint8_t *out = nullptr;
     bool own_out = true;
-    hipEvent_t done = nullptr;
+    hipEvent_t start = nullptr;  // before the slot's copy (timing event)
+    hipEvent_t done = nullptr;   // after the slot's decode (timing event)
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     hipStream_t stream = nullptr;  // this slot's copies + decode, in order
@@ -51,12 +52,31 @@ struct mh_stream {
 
 namespace {
 
+// Makes `dev` current for the scope (and restores the caller's device): every
+// stream call may come from any host thread with any current device.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      ok = false;
+      return;
+    }
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 void release(mh_stream *s) {
   if (!s) return;
   for (auto &sl : s->slots) {
     if (sl.exec) (void)hipGraphExecDestroy(sl.exec);
     if (sl.graph) (void)hipGraphDestroy(sl.graph);
     if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.start) (void)hipEventDestroy(sl.start);
     if (sl.stream) (void)hipStreamDestroy(sl.stream);
     (void)hipFree(sl.base);
     (void)hipFree(sl.init);
@@ -119,7 +139,7 @@ int mh_stream_create(const mh_frame *proto, uint64_t codes_capacity, uint32_t n_
         (want_init && hipMalloc(&sl.init, s->nb) != hipSuccess) ||
         (!d_outputs && hipMalloc(&sl.out, s->out_bytes) != hipSuccess) ||
         hipMemset(sl.base, 0, s->off_bytes + s->cap) != hipSuccess ||
-        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&sl.start) != hipSuccess || hipEventCreate(&sl.done) != hipSuccess ||
         hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
       rc = MH_ERR_HIP;
       break;
@@ -181,6 +201,9 @@ int mh_stream_submit(mh_stream *s, const uint8_t *h_codes, uint64_t codes_bytes,
   if (!h_block_init != !s->slots[0].init) return MH_ERR_INVALID_ARG;
   const uint32_t k = s->next;
   mh_stream::Slot &sl = s->slots[k];
+  DeviceGuard dg(s->device);
+  if (!dg.ok) return MH_ERR_HIP;
+  if (hipEventRecord(sl.start, sl.stream) != hipSuccess) return MH_ERR_HIP;
   // copy then decode on the slot's own stream (its previous decode is ahead in it).
   // Host offsets and codes laid out like the slot ([offsets, padded to 16 B][codes]):
   // one DMA; otherwise two
@@ -221,8 +244,19 @@ int mh_stream_wait(mh_stream *s, uint32_t slot) {
   return hipEventSynchronize(s->slots[slot].done) == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
+int mh_stream_slot_time(mh_stream *s, uint32_t slot, float *ms) {
+  if (!s || slot >= s->slots.size() || !ms) return MH_ERR_INVALID_ARG;
+  const mh_stream::Slot &sl = s->slots[slot];
+  if (!sl.used) return MH_ERR_INVALID_ARG;
+  if (hipEventSynchronize(sl.done) != hipSuccess) return MH_ERR_HIP;
+  return hipEventElapsedTime(ms, sl.start, sl.done) == hipSuccess ? MH_OK : MH_ERR_HIP;
+}
+
+int mh_stream_device(mh_stream *s) { return s ? s->device : -1; }
+
 int mh_stream_synchronize(mh_stream *s) {
   if (!s) return MH_ERR_INVALID_ARG;
+  DeviceGuard dg(s->device);
   for (auto &sl : s->slots)
     if (sl.stream && hipStreamSynchronize(sl.stream) != hipSuccess) return MH_ERR_HIP;
   return MH_OK;
@@ -231,7 +265,85 @@ int mh_stream_synchronize(mh_stream *s) {
 int mh_stream_destroy(mh_stream *s) {
   if (!s) return MH_ERR_INVALID_ARG;
   const int rc = mh_stream_synchronize(s);
+  DeviceGuard dg(s->device);
   release(s);
+  return rc;
+}
+
+// ---- stream groups: frames round-robined over several devices (config 5 on N
+// GPUs). One mh_stream per member, each created on its device; a submit goes to
+// the next member in turn with that member's device made current for the call.
+struct mh_stream_group {
+  std::vector<mh_stream *> members;
+  uint32_t next = 0;
+};
+
+int mh_stream_group_create(const mh_frame *protos, uint32_t n_members, const int *devices,
+                           uint64_t codes_capacity, uint32_t slots_per_member,
+                           mh_stream_group **out) {
+  if (!protos || !devices || !out || n_members < 1 || n_members > 64) return MH_ERR_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) return MH_ERR_HIP;
+  for (uint32_t i = 0; i < n_members; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev) return MH_ERR_INVALID_ARG;
+  mh_stream_group *g = new (std::nothrow) mh_stream_group();
+  if (!g) return MH_ERR_CAPACITY;
+  int rc = MH_OK;
+  for (uint32_t i = 0; i < n_members && rc == MH_OK; ++i) {
+    DeviceGuard dg(devices[i]);
+    if (!dg.ok) {
+      rc = MH_ERR_HIP;
+      break;
+    }
+    mh_stream *s = nullptr;
+    rc = mh_stream_create(&protos[i], codes_capacity, slots_per_member, nullptr, &s);
+    if (rc == MH_OK) g->members.push_back(s);
+  }
+  if (rc != MH_OK) {
+    (void)mh_stream_group_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return MH_OK;
+}
+
+int mh_stream_group_submit(mh_stream_group *g, const uint8_t *h_codes, uint64_t codes_bytes,
+                           const uint32_t *h_block_offsets, const uint8_t *h_block_init,
+                           uint32_t *member, uint32_t *slot) {
+  if (!g || g->members.empty()) return MH_ERR_INVALID_ARG;
+  const uint32_t m = g->next;
+  const int rc = mh_stream_submit(g->members[m], h_codes, codes_bytes, h_block_offsets, h_block_init, slot);
+  if (rc != MH_OK) return rc;
+  g->next = (m + 1) % (uint32_t)g->members.size();
+  if (member) *member = m;
+  return MH_OK;
+}
+
+mh_stream *mh_stream_group_member(mh_stream_group *g, uint32_t member) {
+  return (g && member < g->members.size()) ? g->members[member] : nullptr;
+}
+
+uint32_t mh_stream_group_size(const mh_stream_group *g) { return g ? (uint32_t)g->members.size() : 0u; }
+
+int mh_stream_group_synchronize(mh_stream_group *g) {
+  if (!g) return MH_ERR_INVALID_ARG;
+  int rc = MH_OK;
+  for (mh_stream *s : g->members) {
+    const int r = mh_stream_synchronize(s);
+    if (r != MH_OK) rc = r;
+  }
+  return rc;
+}
+
+int mh_stream_group_destroy(mh_stream_group *g) {
+  if (!g) return MH_ERR_INVALID_ARG;
+  int rc = MH_OK;
+  for (mh_stream *s : g->members) {
+    const int r = mh_stream_destroy(s);
+    if (r != MH_OK) rc = r;
+  }
+  delete g;
   return rc;
 }
 

@@ -136,3 +136,25 @@ def test_constants(mh):
     assert L.mh_lut_bytes() % 16 == 0 and L.mh_lut_bytes() >= 2 * 8192
     assert L.mh_codes_bound(100) >= 100 * 2
     assert L.mh_error_string(-3) == b"huffman code longer than 16 bits"
+
+
+def test_stream_group_argument_checks():
+    """mh_stream_group_*: argument validation happens before any HIP call."""
+    import ctypes
+    import metalhuffman_amd as mh
+    from metalhuffman_amd import _native as N
+    L = mh.lib()
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    protos = (N.mh_frame * 1)()
+    assert L.mh_stream_group_create(None, 1, devs, 4096, 2, ctypes.byref(h)) == -1
+    assert L.mh_stream_group_create(protos, 0, devs, 4096, 2, ctypes.byref(h)) == -1
+    assert L.mh_stream_group_create(protos, 1, None, 4096, 2, ctypes.byref(h)) == -1
+    assert L.mh_stream_group_submit(None, None, 0, None, None, None, None) == -1
+    assert L.mh_stream_group_size(None) == 0
+    assert not L.mh_stream_group_member(None, 0)
+    assert L.mh_stream_group_synchronize(None) == -1
+    assert L.mh_stream_group_destroy(None) == -1
+    f = ctypes.c_float()
+    assert L.mh_stream_slot_time(None, 0, ctypes.byref(f)) == -1
+    assert L.mh_stream_device(None) == -1
