@@ -475,6 +475,16 @@ def cpu_baseline(efs, threads=None, target_s=2.0):
            "cpu_model": _cpu_model(), "host_nproc": os.cpu_count()}
     if aff > share:
         out["all_affinity_threads_MBps"] = round(parallel(aff, dec)[0], 1)
+    # the product's own CPU frame decoder (mh_decode_frame_cpu: shader semantics to the
+    # raster, block rows over threads) -- informational, not the baseline
+    import metalhuffman_amd as mh
+    for n, key in ((1, "product_cpu_frame_decoder_1thread_MBps"), (share, "product_cpu_frame_decoder_MBps")):
+        mh.decode_frame_cpu(efs[0], n)
+        reps = 4 if n == 1 else 32
+        t0 = time.perf_counter()
+        for i in range(reps):
+            mh.decode_frame_cpu(efs[i % len(efs)], n)
+        out[key] = round(reps * px / (time.perf_counter() - t0) / 1e6, 1)
     return out
 
 

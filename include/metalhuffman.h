@@ -301,6 +301,32 @@ int mh_canonical_codes(const uint8_t canon_header[256], uint16_t codes[256]);
 int mh_build_tables(const uint8_t canon_header[256], mh_lookup_symbol table1[256],
                     mh_lookup_symbol *table2, uint32_t table2_cap, uint32_t *table2_entries);
 
+/* CPU decoders (host, reentrant; never used by the GPU path).
+ * HuffmanUtil::decodeHuffmanBits (HuffmanUtil.cpp:673-823; Huffman.h:30): serial
+ * decode of n_symbols from the MSB-first stream through the single 65536-entry
+ * table (mh_build_single_table); bit_offsets (optional, n_symbols entries) gets
+ * each symbol's starting bit. MH_ERR_CAPACITY where the reference asserts
+ * (numBytesRead + 2 < huffBuffN). */
+int mh_decode_huffman_bits(const mh_lookup_symbol *table, uint64_t n_symbols, const uint8_t *codes,
+                           uint64_t codes_bytes, uint8_t *out, uint32_t *bit_offsets);
+/* HuffmanUtil::decodeHuffmanBitsFromTables (HuffmanUtil.cpp:830-1046; Huffman.h:42,
+ * Huffman.mm:101): the same through the T1/T2 pair (table1_bits = table2_bits = 8,
+ * as the reference's tables are built). */
+int mh_decode_huffman_bits_from_tables(const mh_lookup_symbol *table1, const mh_lookup_symbol *table2,
+                                       uint32_t table2_entries, uint32_t table1_bits, uint32_t table2_bits,
+                                       uint64_t n_symbols, const uint8_t *codes, uint64_t codes_bytes,
+                                       uint8_t *out, uint32_t *bit_offsets);
+/* The CPU twin of mh_decode for one frame: every 8x8 block from its root bit
+ * offset with the shader's semantics (AAPLShaders.metal:241-268: 16-bit window,
+ * T1/T2, delta fold unless MH_FLAG_NO_DELTA, optional per-block init byte), written
+ * into the W x H raster at out_pitch; block rows split over n_threads host threads
+ * (0 or 1: the calling thread). Bytes past codes_bytes read as zero. */
+int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uint64_t codes_bytes,
+                        const mh_lookup_symbol *table1, const mh_lookup_symbol *table2,
+                        uint32_t table2_entries, const uint8_t *block_init, uint32_t width,
+                        uint32_t height, uint32_t flags, uint8_t *out, size_t out_pitch,
+                        uint32_t n_threads);
+
 /* The 8-byte container header HuffmanEncoder::encode emits ahead of the
  * canonical table (HuffmanEncoder.cpp:326-340: u32 LE 0xFFEEEEDD, u32 LE symbol
  * count) and HuffmanUtil::encodeHuffman drops (HuffmanUtil.cpp:1073-1086). */

@@ -31,6 +31,7 @@ EXPORTS = (
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
     "mh_encode_frame_device_async",
     "mh_container_header", "mh_parse_container_header", "mh_check",
+    "mh_decode_huffman_bits", "mh_decode_huffman_bits_from_tables", "mh_decode_frame_cpu",
 )
 
 
@@ -136,6 +137,13 @@ def lib() -> ctypes.CDLL:
         L.mh_canonical_codes.argtypes = [_u8p, _u16p]
         L.mh_build_tables.argtypes = [_u8p, _u8p, _u8p, ctypes.c_uint32, _u32p]
         L.mh_build_single_table.argtypes = [_u8p, _u8p]
+        L.mh_decode_huffman_bits.argtypes = [_u8p, ctypes.c_uint64, _u8p, ctypes.c_uint64, _u8p, _u32p]
+        L.mh_decode_huffman_bits_from_tables.argtypes = [_u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                                         ctypes.c_uint32, ctypes.c_uint64, _u8p,
+                                                         ctypes.c_uint64, _u8p, _u32p]
+        L.mh_decode_frame_cpu.argtypes = [_u32p, _u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_uint32, _u8p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
+                                          ctypes.c_size_t, ctypes.c_uint32]
         L.mh_error_string.argtypes = [ctypes.c_int]
         L.mh_error_string.restype = ctypes.c_char_p
         L.mh_device_count.restype = ctypes.c_int

@@ -33,6 +33,7 @@ SOURCES = {
     "mh_stream.o": ("mh_stream.cpp", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
     "mh_host.o": ("mh_host.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-c"]),
+    "mh_cpu.o": ("mh_cpu.cpp", ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-c"]),
 }
 HEADERS = [os.path.join(ROOT, "include", "metalhuffman.h"), os.path.join(CSRC, "mh_lut.hpp")]
 
@@ -57,7 +58,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 print(" ".join(full), flush=True)
             subprocess.run(full, check=True)
     if force or _stale(LIB, objs):
-        full = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        full = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", LIB] + objs
         if verbose:
             print(" ".join(full), flush=True)
         subprocess.run(full, check=True)
@@ -81,7 +82,7 @@ def build_variant(name: str, defines: list[str], verbose: bool = False,
         subprocess.run(cmd + [f"-D{d}" for d in defines] + [f"-I{CSRC}", path, "-o", o], check=True)
         objs.append(o)
     out = os.path.join(VARIANTS_DIR, f"lib_{name}.so")
-    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", out] + objs, check=True)
     if verbose:
         print(out)
     return out

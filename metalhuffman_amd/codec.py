@@ -160,6 +160,38 @@ class Huffman:
         return (np.zeros(0, np.uint8), canon, codes[: ln.value].copy(),
                 offs[: sym.size // stride].copy())
 
+    # +decodeHuffmanBits:numSymbolsToDecode:huffBuff:huffBuffN:outBuffer:bitOffsetTable:
+    # (Huffman.h:30-35, HuffmanUtil.cpp:673-823). -> (symbols, bitOffsetTable)
+    @staticmethod
+    def decodeHuffmanBits(huffSymbolTable, numSymbolsToDecode: int, huffBuff, bitOffsets: bool = False):
+        table = _u8(huffSymbolTable)
+        if table.size != 65536 * 2:
+            raise ValueError("the single lookup table has 65536 two-byte entries")
+        buf = _u8(huffBuff)
+        out = np.zeros(int(numSymbolsToDecode), np.uint8)
+        offs = np.zeros(int(numSymbolsToDecode), np.uint32) if bitOffsets else None
+        N.check(N.lib().mh_decode_huffman_bits(_p(table), out.size, _p(buf), buf.size, _p(out),
+                                               _p(offs, _u32p) if offs is not None else None),
+                "decodeHuffmanBits")
+        return out, offs
+
+    # +decodeHuffmanBitsFromTables:huffSymbolTable2:table1BitNum:table2BitNum:
+    #  numSymbolsToDecode:huffBuff:huffBuffN:outBuffer:bitOffsetTable: (Huffman.h:42-50,
+    # Huffman.mm:101, HuffmanUtil.cpp:830-1046). -> (symbols, bitOffsetTable)
+    @staticmethod
+    def decodeHuffmanBitsFromTables(huffSymbolTable1, huffSymbolTable2, table1BitNum: int,
+                                    table2BitNum: int, numSymbolsToDecode: int, huffBuff,
+                                    bitOffsets: bool = False):
+        t1, t2, buf = _u8(huffSymbolTable1), _u8(huffSymbolTable2), _u8(huffBuff)
+        if t1.size != 512:
+            raise ValueError("T1 has 256 two-byte entries")
+        out = np.zeros(int(numSymbolsToDecode), np.uint8)
+        offs = np.zeros(int(numSymbolsToDecode), np.uint32) if bitOffsets else None
+        N.check(N.lib().mh_decode_huffman_bits_from_tables(
+            _p(t1), _p(t2), t2.size // 2, int(table1BitNum), int(table2BitNum), out.size, _p(buf), buf.size,
+            _p(out), _p(offs, _u32p) if offs is not None else None), "decodeHuffmanBitsFromTables")
+        return out, offs
+
     @staticmethod
     def containerHeader(n_symbols: int) -> np.ndarray:
         """The 8-byte header HuffmanEncoder::encode emits (HuffmanEncoder.cpp:326-340)
@@ -198,6 +230,8 @@ class Huffman:
     generate_lookup_table = generateLookupTable
     generate_split_lookup_tables = generateSplitLookupTables
     encode_huffman = encodeHuffman
+    decode_huffman_bits = decodeHuffmanBits
+    decode_huffman_bits_from_tables = decodeHuffmanBitsFromTables
     encode_signed_byte_deltas = encodeSignedByteDeltas
     decode_signed_byte_deltas = decodeSignedByteDeltas
 
@@ -239,3 +273,17 @@ def encode_frame(gray: np.ndarray, flags: int = 0, init_zero_delta: bool = False
                                     _p(offs, _u32p), _p(init) if init is not None else None),
             "encode_frame")
     return EncodedFrame(w, h, canon, codes[: ln.value].copy(), offs, init, flags)
+
+
+def decode_frame_cpu(ef: EncodedFrame, threads: int = 1) -> np.ndarray:
+    """CPU twin of the GPU decode for one frame (mh_decode_frame_cpu): the shader
+    semantics per block, straight to the H x W raster, on `threads` host threads."""
+    t1, t2 = ef.tables()
+    out = np.zeros((ef.height, ef.width), np.uint8)
+    offs = np.ascontiguousarray(ef.block_offsets, np.uint32)
+    init = np.ascontiguousarray(ef.block_init, np.uint8) if ef.block_init is not None else None
+    N.check(N.lib().mh_decode_frame_cpu(_p(offs, _u32p), _p(ef.codes), ef.codes.size, _p(t1), _p(t2),
+                                        t2.size // 2, _p(init) if init is not None else None, ef.width,
+                                        ef.height, ef.flags, _p(out), ef.width, int(threads)),
+            "mh_decode_frame_cpu")
+    return out

@@ -1,0 +1,172 @@
+// mh_cpu.cpp -- the product's CPU decoders (host, reentrant, no module state).
+//
+// The reference decodes on the CPU in two places: HuffmanUtil::decodeHuffmanBits
+// (single 64K-entry table, Shared/HuffmanUtil.cpp:673-823) and
+// HuffmanUtil::decodeHuffmanBitsFromTables (the T1/T2 pair the shaders use,
+// :830-1046), both exposed through the ObjC facade (Shared/Huffman.mm:90-130) and run
+// as the renderer's DEBUG self-check (Shared/AAPLRenderer.m:616-650). They decode
+// the whole block-order symbol stream serially and optionally record each
+// symbol's bit offset. mh_decode_frame_cpu is the CPU twin of mh_decode: the
+// shader semantics per 8x8 block from its root bit offset (AAPLShaders.metal:
+// 241-268, delta fold and init byte included) straight into the W x H raster,
+// block rows spread over host threads. None of these is called by the GPU path.
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/metalhuffman.h"
+
+namespace {
+
+// The 16-bit window at bit `pos` (MSB first), bytes past `n` read as zero. The
+// reference reads 3 bytes at pos/8 (HuffmanUtil.cpp:700-770); 4 is the same bits.
+inline uint32_t window16(const uint8_t *codes, uint64_t n, uint64_t pos) {
+  const uint64_t b = pos >> 3;
+  uint32_t w = 0;
+  if (b + 4 <= n) {
+    w = ((uint32_t)codes[b] << 24) | ((uint32_t)codes[b + 1] << 16) | ((uint32_t)codes[b + 2] << 8) |
+        codes[b + 3];
+  } else {
+    for (uint64_t i = 0; i < 4; ++i) w = (w << 8) | (b + i < n ? codes[b + i] : 0u);
+  }
+  return (w << (pos & 7)) >> 16;
+}
+
+// T1/T2 lookup of a 16-bit window exactly as AAPLShaders.metal:159-170 /
+// HuffmanUtil.cpp:961-995: T1 by the top 8 bits; bitWidth 0 escapes to subtable
+// `symbol` of T2 indexed by the low 8 bits. An escape past T2 reads the zero entry.
+inline mh_lookup_symbol split_lookup(const mh_lookup_symbol *t1, const mh_lookup_symbol *t2,
+                                     uint32_t t2_entries, uint32_t pat) {
+  mh_lookup_symbol e = t1[pat >> 8];
+  if (e.bitWidth == 0) {
+    const uint32_t idx = (uint32_t)e.symbol * MH_TABLE2_SIZE + (pat & 0xFFu);
+    e = idx < t2_entries ? t2[idx] : mh_lookup_symbol{0, 0};
+  }
+  return e;
+}
+
+// Every window's {symbol, width} from T1/T2 as one u16 (symbol | width << 8):
+// one lookup per symbol in the frame decoder.
+void flatten(const mh_lookup_symbol *t1, const mh_lookup_symbol *t2, uint32_t t2_entries,
+             uint16_t *flat) {
+  for (uint32_t p = 0; p < 65536; ++p) {
+    const mh_lookup_symbol e = split_lookup(t1, t2, t2_entries, p);
+    flat[p] = (uint16_t)(e.symbol | (e.bitWidth << 8));
+  }
+}
+
+// One block: 64 steps from `root` (the shader's per-fragment loop; its cursor is
+// a 16-bit count of bits read), written as 8 rows of the raster.
+inline void decode_block(const uint16_t *flat, const uint8_t *codes, uint64_t n, uint64_t root,
+                         uint8_t init, bool delta, uint8_t blk[64]) {
+  uint16_t nread = 0;
+  uint8_t prev = init;
+  if ((root >> 3) + 8 + 136 <= n) {
+    // fast path: a 64-bit big-endian window, refilled when fewer than 16 bits remain
+    // (a block's 64 codes span at most 128 bytes)
+    const uint8_t *p = codes + (root >> 3);
+    uint64_t pos = root & 7;  // bits consumed from p
+    for (int k = 0; k < 64; ++k) {
+      const uint64_t byte = pos >> 3;
+      uint64_t w;
+      std::memcpy(&w, p + byte, 8);
+      w = __builtin_bswap64(w) << (pos & 7);
+      const uint16_t e = flat[w >> 48];
+      pos += e >> 8;
+      nread = (uint16_t)(nread + (e >> 8));
+      const uint8_t sym = (uint8_t)e;
+      blk[k] = delta ? (prev = (uint8_t)(prev + sym)) : sym;
+    }
+    return;
+  }
+  for (int k = 0; k < 64; ++k) {
+    const uint16_t e = flat[window16(codes, n, root + nread)];
+    nread = (uint16_t)(nread + (e >> 8));
+    const uint8_t sym = (uint8_t)e;
+    blk[k] = delta ? (prev = (uint8_t)(prev + sym)) : sym;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mh_decode_huffman_bits(const mh_lookup_symbol *table, uint64_t n_symbols, const uint8_t *codes,
+                           uint64_t codes_bytes, uint8_t *out, uint32_t *bit_offsets) {
+  if (!table || !codes || !out) return MH_ERR_INVALID_ARG;
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n_symbols; ++i) {
+    if ((pos >> 3) + 2 >= codes_bytes) return MH_ERR_CAPACITY;  // the reference's DEBUG assert
+    const mh_lookup_symbol e = table[window16(codes, codes_bytes, pos)];
+    if (bit_offsets) bit_offsets[i] = (uint32_t)pos;
+    pos += e.bitWidth;
+    out[i] = e.symbol;
+  }
+  return MH_OK;
+}
+
+int mh_decode_huffman_bits_from_tables(const mh_lookup_symbol *table1, const mh_lookup_symbol *table2,
+                                       uint32_t table2_entries, uint32_t table1_bits, uint32_t table2_bits,
+                                       uint64_t n_symbols, const uint8_t *codes, uint64_t codes_bytes,
+                                       uint8_t *out, uint32_t *bit_offsets) {
+  if (!table1 || !table2 || !codes || !out) return MH_ERR_INVALID_ARG;
+  // the reference's tables are built for 8 + 8 bits (HUFF_TABLE1/2_NUM_BITS,
+  // AAPLShaderTypes.h:109-123; T2 subtables are HUFF_TABLE2_SIZE = 256 entries)
+  if (table1_bits != MH_TABLE1_NUM_BITS || table2_bits != MH_TABLE2_NUM_BITS) return MH_ERR_INVALID_ARG;
+  if (table2_entries < 256 || table2_entries % 256 || table2_entries > MH_TABLE2_MAX_ENTRIES)
+    return MH_ERR_TABLE;
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n_symbols; ++i) {
+    if ((pos >> 3) + 2 >= codes_bytes) return MH_ERR_CAPACITY;
+    const mh_lookup_symbol e = split_lookup(table1, table2, table2_entries, window16(codes, codes_bytes, pos));
+    if (bit_offsets) bit_offsets[i] = (uint32_t)pos;
+    pos += e.bitWidth;
+    out[i] = e.symbol;
+  }
+  return MH_OK;
+}
+
+int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uint64_t codes_bytes,
+                        const mh_lookup_symbol *table1, const mh_lookup_symbol *table2,
+                        uint32_t table2_entries, const uint8_t *block_init, uint32_t width,
+                        uint32_t height, uint32_t flags, uint8_t *out, size_t out_pitch,
+                        uint32_t n_threads) {
+  if (!block_offsets || !codes || !table1 || !table2 || !out) return MH_ERR_INVALID_ARG;
+  if (flags & ~MH_FLAG_NO_DELTA) return MH_ERR_INVALID_ARG;
+  if (!width || !height || width > MH_MAX_DIM || height > MH_MAX_DIM) return MH_ERR_DIMS;
+  if (table2_entries < 256 || table2_entries % 256 || table2_entries > MH_TABLE2_MAX_ENTRIES)
+    return MH_ERR_TABLE;
+  if (out_pitch < width) return MH_ERR_CAPACITY;
+  const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
+  const bool delta = !(flags & MH_FLAG_NO_DELTA);
+  std::vector<uint16_t> flat(65536);
+  flatten(table1, table2, table2_entries, flat.data());
+  const auto rows = [&](uint32_t by0, uint32_t by1) {
+    uint8_t blk[64];
+    for (uint32_t by = by0; by < by1; ++by)
+      for (uint32_t bx = 0; bx < bw; ++bx) {
+        const uint32_t b = by * bw + bx;
+        decode_block(flat.data(), codes, codes_bytes, block_offsets[b], block_init ? block_init[b] : 0,
+                     delta, blk);
+        const uint32_t nx = std::min(8u, width - bx * 8);
+        for (uint32_t r = 0; r < 8 && by * 8 + r < height; ++r)
+          std::memcpy(out + (size_t)(by * 8 + r) * out_pitch + bx * 8, blk + r * 8, nx);
+      }
+  };
+  uint32_t nt = std::max(1u, std::min(n_threads ? n_threads : 1u, bh));
+  if (nt == 1) {
+    rows(0, bh);
+    return MH_OK;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint32_t a = (uint32_t)((uint64_t)bh * t / nt), z = (uint32_t)((uint64_t)bh * (t + 1) / nt);
+    th.emplace_back(rows, a, z);
+  }
+  for (auto &x : th) x.join();
+  return MH_OK;
+}
+
+}  // extern "C"

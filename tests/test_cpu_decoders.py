@@ -1,0 +1,100 @@
+"""The product's CPU decoders (csrc/mh_cpu.cpp) against the oracle's restatements
+and the reference's own fixtures: HuffmanUtil::decodeHuffmanBits (single table,
+HuffmanUtil.cpp:673-823), decodeHuffmanBitsFromTables (T1/T2, :830-1046, also the
+Huffman.mm:101 facade) and the threaded CPU frame decoder (shader semantics,
+AAPLShaders.metal:241-268). Bit-exact symbols, bit offsets and rasters."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import fibonacci_deltas, golden, image_from_block_deltas
+
+
+def _frames(mh, bigbridge):
+    from metalhuffman_amd import frames as F
+    yield "bigbridge", mh.encode_frame(bigbridge), bigbridge
+    crop = F.crop(bigbridge, 1001, 777)
+    yield "crop_init", mh.encode_frame(crop, init_zero_delta=True), crop
+    r = F.uniform_random(256, 320, 5)
+    yield "random", mh.encode_frame(r), r
+    d = fibonacci_deltas(17, 256 * 256, seed=9)
+    img = image_from_block_deltas(d, 256, 256)
+    yield "fib16", mh.encode_frame(img), img
+    raw = fibonacci_deltas(15, 128 * 64, seed=2).reshape(64, 128)
+    yield "no_delta", mh.encode_frame(raw, flags=mh.MH_FLAG_NO_DELTA), raw
+
+
+def test_serial_decoders_match_oracle(mh, oracle, bigbridge):
+    for name, ef, img in _frames(mh, bigbridge):
+        t1, t2 = ef.tables()
+        nsym = ef.n_blocks * 64
+        want, want_offs = oracle.decode_from_tables(t1, t2, nsym, ef.codes, want_offsets=True)
+        got, offs = mh.Huffman.decodeHuffmanBitsFromTables(t1, t2, 8, 8, nsym, ef.codes, bitOffsets=True)
+        assert np.array_equal(got, want), name
+        assert np.array_equal(offs, want_offs), name
+        assert np.array_equal(offs[::64], ef.block_offsets), name
+        single = mh.Huffman.generateLookupTable(ef.canon)
+        got1, offs1 = mh.Huffman.decodeHuffmanBits(single, nsym, ef.codes, bitOffsets=True)
+        assert np.array_equal(got1, want) and np.array_equal(offs1, want_offs), name
+
+
+def test_frame_decoder_matches_oracle_and_input(mh, oracle, bigbridge):
+    for name, ef, img in _frames(mh, bigbridge):
+        t1, t2 = ef.tables()
+        ref = oracle.decode_frame_shader(ef.block_offsets, ef.codes, t1, t2, ef.width, ef.height,
+                                         block_init=ef.block_init, delta=not (ef.flags & 1))
+        for threads in (1, 3, 8):
+            out = mh.decode_frame_cpu(ef, threads)
+            assert np.array_equal(out, ref), (name, threads)
+            assert np.array_equal(out, img), (name, threads)
+
+
+def test_frame_decoder_zero_width_and_garbage(mh, oracle, bigbridge):
+    """{0,0} windows (the reference's dummy T2 subtable) repeat prev without
+    advancing; a garbage stream decodes exactly like the oracle's shader restatement."""
+    from metalhuffman_amd import codec as C
+    img = np.zeros((24, 40), np.uint8)
+    ef = mh.encode_frame(img)
+    bad = C.EncodedFrame(ef.width, ef.height, ef.canon, np.full_like(ef.codes, 0xFF), ef.block_offsets)
+    t1, t2 = bad.tables()
+    ref = oracle.decode_frame_shader(bad.block_offsets, bad.codes, t1, t2, 40, 24)
+    assert np.array_equal(mh.decode_frame_cpu(bad, 2), ref)
+    ef = mh.encode_frame(np.ascontiguousarray(bigbridge[:768, :1024]))
+    # zero tail: both sides read past the payload of a garbage stream (the oracle
+    # has no bound), so give them defined zero bytes there
+    junk = np.concatenate([np.random.default_rng(1).integers(0, 256, ef.codes.size, dtype=np.uint8),
+                           np.zeros(256, np.uint8)])
+    g = C.EncodedFrame(ef.width, ef.height, ef.canon, junk, ef.block_offsets)
+    t1, t2 = g.tables()
+    assert np.array_equal(mh.decode_frame_cpu(g, 4),
+                          oracle.decode_frame_shader(g.block_offsets, g.codes, t1, t2, 1024, 768))
+
+
+def test_reference_encoder_buffers(mh):
+    """The reference encoder's own buffers (golden.json) through the product's CPU
+    decoders reproduce the reference-held pixels."""
+    from metalhuffman_amd import codec as C
+    for name, fx in golden()["small_frames"].items():
+        w, h = fx["width"], fx["height"]
+        canon = np.zeros(256, np.uint8)
+        for k, v in fx["canon"].items():
+            canon[int(k)] = v
+        codes = np.frombuffer(bytes.fromhex(fx["codes_hex"]), np.uint8)
+        ef = C.EncodedFrame(w, h, canon, np.concatenate([codes, np.zeros(2, np.uint8)]),
+                            np.array(fx["block_offsets"], np.uint32))
+        assert np.array_equal(mh.decode_frame_cpu(ef), np.array(fx["pixels"], np.uint8).reshape(h, w)), name
+
+
+def test_argument_errors(mh):
+    L = mh.lib()
+    assert L.mh_decode_huffman_bits(None, 1, None, 0, None, None) == -1
+    t1 = np.zeros(512, np.uint8)
+    t2 = np.zeros(512, np.uint8)
+    out = np.zeros(4, np.uint8)
+    buf = np.zeros(2, np.uint8)
+    with pytest.raises(mh.MHError):  # reads past the buffer where the reference asserts
+        mh.Huffman.decodeHuffmanBitsFromTables(t1, t2, 8, 8, 4, buf)
+    with pytest.raises(mh.MHError):
+        mh.Huffman.decodeHuffmanBitsFromTables(t1, t2, 9, 7, 4, np.zeros(16, np.uint8))
+    del out
