@@ -75,10 +75,17 @@ def algo_bytes(efs, t2_bytes: int) -> int:
     return per + 512 + t2_bytes
 
 
+def algo_read_bytes(efs, t2_bytes: int) -> int:
+    """The read share of algo_bytes (codes + offsets + tables): what north_star's
+    "HBM read roofline" fraction is computed from."""
+    return sum(ef.payload_bytes + 4 * ef.n_blocks for ef in efs) + 512 + t2_bytes
+
+
 class Workload:
     """A set of launches (one DeviceFrames each) cycled over by the steps."""
 
-    def __init__(self, name, launches, tables, pixels_per_launch, bytes_per_launch, device, refs=None):
+    def __init__(self, name, launches, tables, pixels_per_launch, bytes_per_launch, device, refs=None,
+                 read_bytes=None):
         from metalhuffman_amd import decoder as D
         self.D = D
         self.name = name
@@ -87,6 +94,8 @@ class Workload:
         self.tables = tables
         self.pixels = pixels_per_launch
         self.bytes = bytes_per_launch
+        self.read_bytes = read_bytes
+        self.ungated_wall = None
         self.device = device
         self.outs = [torch.empty((f.n_frames, f.height, (f.width + 7) // 8 * 8), dtype=torch.uint8,
                                  device=device) for f in launches]
@@ -113,7 +122,7 @@ class Workload:
                 n += 1
         return n
 
-    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=50.0):
+    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=50.0, gate=True):
         """Timed region: `steps` launches (one hipGraph replay, or eager), bracketed by
         barrier + synchronize; wall = max over ranks.
         Kernel durations: the same `steps` launches issued eagerly right after, each
@@ -168,27 +177,55 @@ class Workload:
             wb.record()
             torch.cuda.synchronize(dev)
             print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        r0.record()
-        if graph is not None:
-            graph.replay()
+        def timed(gated):
+            """One timed region of exactly `steps` launches. Gated: the launches are
+            enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
+            opening synchronize, and the clock starts when the host opens it -- every
+            decode runs inside the region, the host's enqueue latency does not."""
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            if gated:
+                GATE.arm(torch.cuda.current_stream(dev).cuda_stream)
+            if gated or graph is not None:
+                r0.record()
+                if graph is not None:
+                    graph.replay()
+                else:
+                    for i in range(steps):
+                        self.launch(i)
+                r1.record()
+            # (no barrier while a gate is armed: an RCCL barrier would queue behind it;
+            # each rank times its own region, the max over ranks is taken below)
+            t0 = time.perf_counter()
+            if gated:
+                GATE.open()
+            else:
+                r0.record()
+                if graph is not None:
+                    graph.replay()
+                else:
+                    for i in range(steps):
+                        self.launch(i)
+                r1.record()
+            torch.cuda.synchronize(dev)
+            w = time.perf_counter() - t0
+            if world > 1:
+                dist.barrier()
+                on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+                t = torch.tensor([w], dtype=torch.float64, device=on)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                w = float(t.item())
+            return w, r0.elapsed_time(r1)
+
+        if gate and GATE.ok():
+            timed(True)  # the gate's own first launch off the clock
+            wall, region_ms = timed(True)
+            self.ungated_wall, _ = timed(False)
         else:
-            for i in range(steps):
-                self.launch(i)
-        r1.record()
-        torch.cuda.synchronize(dev)
-        wall = time.perf_counter() - t0
-        if world > 1:
-            dist.barrier()
-            on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-            t = torch.tensor([wall], dtype=torch.float64, device=on)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            wall = float(t.item())
-        region_ms = r0.elapsed_time(r1)
+            wall, region_ms = timed(False)
+            self.ungated_wall = None
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
         for i in range(steps):
@@ -218,7 +255,45 @@ def measured_traffic(workload: str):
 ACHIEVABLE = {}  # filled from hbm_probe() before the roofline lines (rank 0, N=1)
 
 
-def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
+class _Gate:
+    """The timed-region launch gate (scripts/micro/liblaunch_gate.so): a one-wave
+    kernel polling a host-mapped flag, so the K launches can be enqueued before the
+    clock starts. MH_BENCH_GATE=0 times the plain (ungated) region only."""
+
+    def __init__(self):
+        self.lib = None
+        self.h = self.d = None
+
+    def ok(self) -> bool:
+        if os.environ.get("MH_BENCH_GATE", "1") == "0":
+            return False
+        if self.lib is None:
+            import ctypes
+            path = os.path.join(ROOT, "scripts", "micro", "liblaunch_gate.so")
+            if not os.path.exists(path):
+                return False
+            lib = ctypes.CDLL(path)
+            lib.gate_create.argtypes = [ctypes.POINTER(ctypes.c_void_p)] * 2
+            lib.gate_arm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+            lib.gate_open.argtypes = [ctypes.c_void_p]
+            h, d = ctypes.c_void_p(), ctypes.c_void_p()
+            if lib.gate_create(ctypes.byref(h), ctypes.byref(d)) != 0:
+                return False
+            self.lib, self.h, self.d = lib, h, d
+        return True
+
+    def arm(self, stream: int) -> None:
+        if self.lib.gate_arm(self.h, self.d, stream, 200_000) != 0:  # opens by itself after 200 ms
+            raise RuntimeError("launch gate: kernel launch failed")
+
+    def open(self) -> None:
+        self.lib.gate_open(self.h)
+
+
+GATE = _Gate()
+
+
+def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None, read_bytes=None):
     """achieved = algorithmic bytes of one launch / the launch's average duration,
     the latter from the HIP events bracketing the timed hipGraph replay on its
     stream (the K kernels run back to back there, so region / K is the kernel
@@ -236,6 +311,16 @@ def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None):
     if mix:
         r["achievable_mix_GBps"] = mix
         r["frac_of_achievable"] = round(ach / mix, 4)
+    if read_bytes:
+        # north_star's "per-GPU HBM read roofline": the launch's read bytes (codes,
+        # offsets, tables) over its duration, against the spec and the measured
+        # read-only stream
+        rd = read_bytes / avg_s / 1e9
+        r["read_bytes_per_launch"] = int(read_bytes)
+        r["read_achieved"] = round(rd, 1)
+        r["read_frac"] = round(rd / HBM_PEAK_GBS, 4)
+        if ACHIEVABLE.get("read_GBps"):
+            r["read_frac_of_achievable"] = round(rd / ACHIEVABLE["read_GBps"], 4)
     if eager_ms:
         # one launch at a time with an event pair each (includes launch latency)
         r["eager_launch_us_median"] = round(float(np.median(eager_ms)) * 1e3, 3)
@@ -574,14 +659,16 @@ def main(argv=None) -> int:
     def frame_workload():
         launches = [pack([ef]) for ef in efs]
         return Workload("frame", launches, tables, bb.size, algo_bytes(efs[:1], t2_bytes), dev,
-                        refs=[dimgs[i:i + 1] for i in range(len(efs))])
+                        refs=[dimgs[i:i + 1] for i in range(len(efs))],
+                        read_bytes=algo_read_bytes(efs[:1], t2_bytes))
 
     def batch_workload(nb):
         starts = [i for i in range(0, len(efs), nb) if i + nb <= len(efs)] or [0]
         groups = [efs[i:i + nb] for i in starts]
         launches = [pack(g) for g in groups]
         return Workload(f"batch{nb}", launches, tables, nb * bb.size, algo_bytes(groups[0], t2_bytes), dev,
-                        refs=[dimgs[i:i + nb] for i in starts])
+                        refs=[dimgs[i:i + nb] for i in starts],
+                        read_bytes=algo_read_bytes(groups[0], t2_bytes))
 
     def tile_workload(random=False):
         # config 3: BigBridge mirror tile (primary) or uniform random bytes (stress:
@@ -594,7 +681,8 @@ def main(argv=None) -> int:
         launches = [pack([ef]) for ef in tefs]
         name = "tile8192_random" if random else "tile8192"
         return Workload(name, launches, ttabs, base.size, algo_bytes(tefs[:1], ttabs.table2.numel()), dev,
-                        refs=[torch.from_numpy(im).to(dev).unsqueeze(0) for im in imgs])
+                        refs=[torch.from_numpy(im).to(dev).unsqueeze(0) for im in imgs],
+                        read_bytes=algo_read_bytes(tefs[:1], ttabs.table2.numel()))
 
     if args.workload == "frame":
         wl = frame_workload()
@@ -635,9 +723,16 @@ def main(argv=None) -> int:
                    "frames_per_step_per_gpu": int(wl.launches[0].n_frames),
                    "parallelism": f"frame-sharded x{world}", "launch": "hipGraph" if not args.no_graph else "eager"},
         "mpixels_per_s": round(value, 1),
-        "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload),
+        "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload, wl.read_bytes),
         "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
+        "timing": ("gated: the K launches are enqueued behind a host-opened launch gate before "
+                   "the clock starts (scripts/micro/launch_gate.hip); every decode runs inside "
+                   "the timed region" if wl.ungated_wall is not None else "plain"),
     }
+    if wl.ungated_wall is not None:
+        # the same K launches timed the plain way (enqueue latency inside the clock)
+        result["ungated_ms_per_step"] = round(wl.ungated_wall / args.steps * 1e3, 5)
+        result["ungated_value"] = round(world * wl.pixels / (wl.ungated_wall / args.steps) / 1e6, 1)
     result["frames_verified"] = frames_verified
     if ranks_ok is not None:
         result["ranks_verified"] = ranks_ok
@@ -663,7 +758,7 @@ def main(argv=None) -> int:
                             "ms_per_step": round(wall2 / steps * 1e3, 4),
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
                             "frames_verified": nver,
-                            "roofline": roofline(w2.bytes, reg2, steps, kms2, key)}
+                            "roofline": roofline(w2.bytes, reg2, steps, kms2, key, w2.read_bytes)}
             del w2
         extras["hbm_copy"] = copy_bandwidth(dev)  # achievable HBM rate beside the 8 TB/s spec
         if ACHIEVABLE:

@@ -110,17 +110,20 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
 
 PROBE_SRC = os.path.join(ROOT, "scripts", "micro", "hbm_probe.hip")
 PROBE_LIB = os.path.join(ROOT, "scripts", "micro", "libhbm_probe.so")
+GATE_SRC = os.path.join(ROOT, "scripts", "micro", "launch_gate.hip")
+GATE_LIB = os.path.join(ROOT, "scripts", "micro", "liblaunch_gate.so")
 
 
 def build_probe(force: bool = False, verbose: bool = False) -> str:
-    """The achievable-HBM probe bench.py reports beside the roofline (measurement
-    infrastructure, not the decoder): scripts/micro/libhbm_probe.so."""
-    if force or _stale(PROBE_LIB, [PROBE_SRC]):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared",
-               "-o", PROBE_LIB, PROBE_SRC]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+    """bench.py's measurement infrastructure (not the decoder): the achievable-HBM
+    probe reported beside the roofline (scripts/micro/libhbm_probe.so) and the
+    timed-region launch gate (scripts/micro/liblaunch_gate.so)."""
+    for src, lib in ((PROBE_SRC, PROBE_LIB), (GATE_SRC, GATE_LIB)):
+        if force or _stale(lib, [src]):
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-o", lib, src]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
     return PROBE_LIB
 
 

@@ -1,0 +1,57 @@
+// launch_gate.hip -- bench.py's timed-region gate (measurement infrastructure, not
+// part of the decoder). The K timed launches are enqueued behind a one-wave kernel
+// that polls a host-mapped flag; the clock starts when the host sets the flag. Every
+// timed decode still runs inside the timed region -- only the host's enqueue latency
+// (graph launch API + doorbell, ~20 us measured at 20 steps) moves before it.
+//
+// The poll ends by itself after `max_us` (no flag: the gate opens late, never hangs).
+// Built by metalhuffman_amd.build.build_probe() into scripts/micro/liblaunch_gate.so.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+namespace {
+
+__global__ void __launch_bounds__(64) gate_kernel(const unsigned *flag, unsigned long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz counter
+  // system-scope atomic loads: vector memory reads of the host-mapped word
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// A host-mapped, coherent flag word; *host_ptr is written by the host, the kernel
+// polls *dev_ptr.
+int gate_create(unsigned **host_ptr, unsigned **dev_ptr) {
+  void *h = nullptr;
+  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return -1;
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return -1;
+  }
+  *reinterpret_cast<volatile unsigned *>(h) = 0u;
+  *host_ptr = static_cast<unsigned *>(h);
+  *dev_ptr = static_cast<unsigned *>(d);
+  return 0;
+}
+
+// Close the flag and enqueue the gate on `stream`; later work on it waits behind.
+int gate_arm(unsigned *host_ptr, const unsigned *dev_ptr, void *stream, unsigned max_us) {
+  __atomic_store_n(host_ptr, 0u, __ATOMIC_SEQ_CST);
+  hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dev_ptr,
+                     (unsigned long long)max_us * 100ull);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void gate_open(unsigned *host_ptr) { __atomic_store_n(host_ptr, 1u, __ATOMIC_SEQ_CST); }
+
+void gate_destroy(unsigned *host_ptr) { (void)hipHostFree(host_ptr); }
+
+}  // extern "C"
