@@ -81,6 +81,11 @@ def algo_read_bytes(efs, t2_bytes: int) -> int:
     return sum(ef.payload_bytes + 4 * ef.n_blocks for ef in efs) + 512 + t2_bytes
 
 
+# A/B switch for decode-only flags (e.g. 2 = MH_FLAG_LANE_PAIRS); the parity guard
+# (Workload.verify) decodes through the same flags before anything is timed
+DECODE_FLAGS = int(os.environ.get("MH_BENCH_DECODE_FLAGS", "0"), 0)
+
+
 class Workload:
     """A set of launches (one DeviceFrames each) cycled over by the steps."""
 
@@ -102,7 +107,7 @@ class Workload:
 
     def launch(self, i):
         j = i % len(self.launches)
-        self.D.decode(self.launches[j], self.tables, self.outs[j])
+        self.D.decode(self.launches[j], self.tables, self.outs[j], extra_flags=DECODE_FLAGS)
 
     def verify(self) -> int:
         """Parity guard before any timing: every resident launch is decoded once and

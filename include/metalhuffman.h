@@ -66,6 +66,12 @@ extern "C" {
 /* decode flags */
 #define MH_FLAG_NO_DELTA 0x1u    /* IMPL_DELTAS_BEFORE_HUFF_ENCODING off
                                     (AAPLShaders.metal:263-265): emit symbols raw */
+#define MH_FLAG_LANE_PAIRS 0x2u  /* experimental (A/B): small launches (one frame)
+                                    decode each block with a lane pair -- one lane
+                                    from the block start, one speculatively from
+                                    its middle bit, re-synchronised through
+                                    ds_bpermute; same output. Ignored by batch
+                                    launches */
 
 /* Shared/HuffmanLookupSymbol.h:7-10: 2-byte entry. In T1, bitWidth == 0 marks
  * an escape whose `symbol` is the T2 subtable index (HuffmanUtil.cpp:639-646). */

@@ -12,12 +12,12 @@ of mdejong/MetalHuffman).
   * stream                          streaming from host memory (config 5)
   * dist                            frame sharding, single-frame bands, table broadcast
 """
-from ._native import EXPORTS, LIB_PATH, MH_CODES_PAD, MH_FLAG_NO_DELTA, MHError, lib
+from ._native import EXPORTS, LIB_PATH, MH_CODES_PAD, MH_FLAG_LANE_PAIRS, MH_FLAG_NO_DELTA, MHError, lib
 from .codec import (BLOCK_DIM, EncodedFrame, Huffman, block_grid, decode_frame_cpu, encode_frame, merge_blocks,
                     split_blocks)
 
 __all__ = [
-    "EXPORTS", "LIB_PATH", "MH_CODES_PAD", "MH_FLAG_NO_DELTA", "MHError", "lib", "BLOCK_DIM",
+    "EXPORTS", "LIB_PATH", "MH_CODES_PAD", "MH_FLAG_LANE_PAIRS", "MH_FLAG_NO_DELTA", "MHError", "lib", "BLOCK_DIM",
     "EncodedFrame", "Huffman", "block_grid", "decode_frame_cpu", "encode_frame", "merge_blocks", "split_blocks",
 ]
 __version__ = "0.1.0"

@@ -73,6 +73,9 @@ namespace {
 #ifndef MH_SMALL_MASKED         // small-launch kernel: masked refill reads (kSpec 0 only)
 #define MH_SMALL_MASKED 0
 #endif
+#ifndef MH_LP_MIN_BITS          // lane-pair variant: blocks shorter than 2x this decode on one lane
+#define MH_LP_MIN_BITS 16
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -818,6 +821,283 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 #endif
 }
 
+// ---- lane-pair variant of the small-launch kernel (MH_FLAG_LANE_PAIRS, A/B) -------
+// north_star's lane-group cursor: each 8x8 block is decoded by two lanes of one
+// wave, lanes l and l ^ 32 (32 blocks per wave, so twice the waves of the small
+// kernel). Lane A starts at the block's first bit (AAPLShaders.metal:241-268);
+// lane B starts speculatively at the block's middle bit M = off + len/2 (len from
+// the next block's offset) and records which bits in [M, M + 64) start one of its
+// symbols. Huffman paths re-synchronise: once A reaches a bit >= M that B also
+// started a symbol at, the two paths coincide from there on, so A stops and B's
+// symbols from that point are the block's remaining symbols. The cursor hand-off
+// (B's position and start mask to A, A's stop count to B) goes through
+// ds_bpermute. A block whose lanes never meet (or disagree with the block end) is
+// finished serially by lane A. Each lane writes its running output bytes into a
+// per-lane LDS row; the block's rows are assembled from the two (B's bytes rebased
+// by the running delta sum at the meeting point) and stored 8 bytes per row.
+#ifndef MH_LP_WAVES
+#define MH_LP_WAVES 4
+#endif
+constexpr int kLpWaves = MH_LP_WAVES;
+constexpr int kLpStageBytes = 3712;   // >= 15 + 32 blocks x 64 x 14 bits / 8 + 24, 16-B multiple
+constexpr int kLpOutStride = 68;      // bytes per lane row (17 dwords: lanes spread over banks)
+__shared__ __attribute__((aligned(16))) uint16_t s_lp_lut[kLut14Entries];
+__shared__ __attribute__((aligned(16))) uint8_t s_lp_stage[kLpWaves * kLpStageBytes];
+__shared__ __attribute__((aligned(16))) uint8_t s_lp_out[kLpWaves * 64 * kLpOutStride];
+
+// Bit cursor over a wave's staged span (byte offsets into the stage).
+template <int kBits>
+struct LpCur {
+  static constexpr uint32_t kCur = 127u - (uint32_t)kBits;
+  static constexpr uint32_t kMask = (2u << kBits) - 2u;
+  static constexpr uint32_t kRefillAt = kCur - 32u;
+  uint32_t hi, lo, nw, wa, wbits, S;
+  __device__ __forceinline__ void init(const uint8_t *stage, uint32_t bit, uint32_t prev) {
+    wa = (bit >> 5) * 4u;
+    wbits = (bit >> 5) * 32u;
+    S = (prev << 8) + kCur - (bit & 31u);
+    hi = word_at(stage + wa);
+    lo = word_at(stage + wa + 4);
+    nw = word_at(stage + wa + 8);
+  }
+  __device__ __forceinline__ uint32_t pos() const { return wbits + kCur - (S & 0xFFu); }
+  // one symbol (the small kernel's step, refilled before every symbol); returns
+  // the output byte: the running delta sum, or the raw symbol
+  template <bool kDelta, bool kEsc>
+  __device__ __forceinline__ uint32_t step(const uint8_t *stage, const uint8_t *lut) {
+    if ((S & 0xFFu) <= kRefillAt) {
+      hi = lo;
+      lo = nw;
+      wa += 4u;
+      wbits += 32u;
+      S += 32u;
+      nw = word_at(stage + wa + 8);
+    }
+    const uint64_t x = (((uint64_t)hi) << 32) | lo;
+    uint32_t e = *reinterpret_cast<const uint16_t *>(lut + ((uint32_t)(x >> (S & 63u)) & kMask));
+    if constexpr (kEsc) {
+      if (e < kEscapeBelow) {
+        const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;
+        e = *reinterpret_cast<const uint16_t *>(lut + 2u * (kL1Entries + ((e & 0xFFu) << kL2Bits) + x3));
+      }
+    }
+    S += e;
+    return kDelta ? ((S >> 8) & 0xFFu) : (((e + 0xFFu) >> 8) & 0xFFu);
+  }
+};
+
+__device__ __forceinline__ uint32_t lane_xchg(uint32_t lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ 32u) << 2), (int)v);
+}
+
+template <bool kDelta, int kBits, bool kEsc>
+__device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *lut, uint8_t *row_a,
+                                          uint8_t *row_b, uint32_t lane, bool valid, uint32_t p,
+                                          uint32_t mid, uint32_t end, bool exact_end, bool spec,
+                                          uint32_t init, __amdgpu_buffer_rsrc_t out, uint32_t row0,
+                                          uint32_t pitch) {
+  const bool is_b = lane >= 32u;
+  uint8_t *row = is_b ? row_b : row_a;
+  LpCur<kBits> c;
+  c.init(stage, is_b ? mid : p, is_b ? 0u : init);
+  bool act = valid && (!is_b || spec);
+  bool checking = valid && spec;  // A: still looking for the meeting point
+  bool synced = false;
+  uint32_t n = 0, ia = 64, jb = 0, nb_b = 0, end_b = 0, target = 64;
+  uint64_t mask = 0;  // B: symbol starts at mid + k, k < 64
+
+  while (__ballot(act)) {  // wave-uniform
+    const uint32_t pb = c.pos();
+    if (is_b && act && pb - mid < 64u) mask |= 1ull << (pb - mid);
+    const bool need_a = !is_b && act && checking && pb >= mid;
+    const bool need_b = is_b && act && !exact_end;
+    if (__ballot(need_a || need_b)) {
+      // A publishes B's stop count once met; B its cursor (bit 31: finished) and mask
+      const uint32_t w0 = is_b ? (act ? pb : (0x80000000u | end_b)) : (synced ? 0x80000000u | (jb + 64u - ia) : 0u);
+      const uint32_t x0 = lane_xchg(lane, w0);
+      const uint32_t x1 = lane_xchg(lane, (uint32_t)mask);
+      const uint32_t x2 = lane_xchg(lane, (uint32_t)(mask >> 32));
+      if (need_a) {
+        const uint32_t rel = pb - mid;
+        if (rel >= 64u) {
+          checking = false;  // never met within the window: A decodes the whole block
+        } else if ((x0 >> 31) || (x0 & 0x7FFFFFFFu) >= pb) {  // B's mask is final up to pb
+          const uint64_t mb = (((uint64_t)x2) << 32) | x1;
+          if ((mb >> rel) & 1u) {
+            synced = true;
+            checking = false;
+            act = false;
+            ia = n;
+            jb = (uint32_t)__builtin_popcountll(mb & ((1ull << rel) - 1u));
+          }
+        }
+      }
+      if (need_b && (x0 >> 31)) target = x0 & 0x7Fu;
+    }
+    if (act) {
+      row[n] = (uint8_t)c.template step<kDelta, kEsc>(stage, lut);
+      ++n;
+      if (is_b) {
+        const uint32_t pa = c.pos();
+        if ((exact_end && pa >= end) || n >= target || n >= 64u) {
+          act = false;
+          nb_b = n;
+          end_b = pa;
+        }
+      } else if (n >= 64u) {
+        act = false;
+      }
+    }
+  }
+  // Meeting point consistent with B's end? (B must reach the block end exactly
+  // after jb + 64 - ia symbols.) Otherwise A finishes the block from where it stopped.
+  {
+    const uint32_t wa = synced ? (0x80000000u | (ia << 8) | jb) : 0u;
+    const uint32_t wb = nb_b | ((!exact_end || end_b == end) ? 0x80000000u : 0u);
+    const uint32_t x = lane_xchg(lane, is_b ? wb : wa);
+    bool repair = false;
+    if (!is_b && synced) {
+      const bool ok = (x >> 31) && (x & 0x7Fu) == jb + 64u - ia;
+      if (!ok) {
+        synced = false;
+        repair = true;
+      }
+    }
+    while (__ballot(repair)) {
+      if (repair) {
+        row[n] = (uint8_t)c.template step<kDelta, kEsc>(stage, lut);
+        if (++n >= 64u) repair = false;
+      }
+    }
+  }
+  // Assemble and store: lane A rows 0-3, lane B rows 4-7 of the block.
+  const uint32_t fin = lane_xchg(lane, synced ? (0x80000000u | (ia << 8) | jb) : 0u);
+  const uint32_t f = is_b ? fin : (synced ? (0x80000000u | (ia << 8) | jb) : 0u);
+  const bool split = (f >> 31) != 0;
+  const uint32_t i_a = split ? (f >> 8) & 0x7Fu : 64u;
+  const uint32_t j_b = f & 0x7Fu;
+  wave_sync();  // every lane's row bytes -> reads
+  const uint32_t pa = i_a ? row_a[i_a - 1u] : init;
+  const uint32_t lb = j_b ? row_b[j_b - 1u] : 0u;
+  const uint32_t cadd = kDelta ? ((pa - lb) & 0xFFu) : 0u;
+  const uint32_t r0 = is_b ? 4u : 0u;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    uint32_t w[2] = {0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t i = (r0 + r) * 8u + k;
+      const uint32_t v = i < i_a ? row_a[i] : ((row_b[i - i_a + j_b] + cadd) & 0xFFu);
+      w[k >> 2] |= v << (8u * (k & 3u));
+    }
+    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+    v2u32 v;
+    v.x = w[0];
+    v.y = w[1];
+    const uint32_t off = valid ? row0 + (r0 + r) * pitch : 0xFFFFFFF0u;
+    __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
+  }
+}
+
+template <bool kDelta>
+__global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const DecodeArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t bl = lane & 31u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t *stage = s_lp_stage + wave * kLpStageBytes;
+  uint8_t *row_a = s_lp_out + (wave * 64u + bl) * kLpOutStride;
+  uint8_t *row_b = row_a + 32u * kLpOutStride;
+  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lp_lut);
+  const uint8_t *prepared = reinterpret_cast<const uint8_t *>(a.lut);
+  const uint32_t max_len = *reinterpret_cast<const uint32_t *>(prepared + kMaxLenOff);
+  const bool l14 = max_len <= (uint32_t)kLut14Bits;
+
+  // header: 32-block tiles (a.tiles_per_frame / a.total_tiles count them)
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(min(blockIdx.x * kLpWaves + wave, a.total_tiles));
+  const bool live = tile < a.total_tiles;
+  const uint32_t fi = live ? tile / a.tiles_per_frame : 0u;
+  const uint32_t b0 = live ? (tile - fi * a.tiles_per_frame) * 32u : 0u;
+  const uint32_t b = b0 + bl;
+  const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(a.offsets + (uint64_t)fi * a.nb, live ? a.nb * 4u : 0u);
+  const uint32_t off = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(b * 4u), 0, 0);
+  const uint32_t nxt = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(b * 4u + 4u), 0, 0);
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t rf = uniform_rsrc(
+      a.frame_off ? (const void *)a.frame_off : (const void *)a.offsets,
+      (live && a.frame_off) ? 0x7FFFFFF0u : 0u);
+  const v2u32 fo = __builtin_amdgcn_raw_buffer_load_b64(rf, (int)((fi + (lane & 1u)) * 8u), 0, 0);
+  const __amdgpu_buffer_rsrc_t ri = uniform_rsrc(
+      a.block_init ? (const void *)(a.block_init + (uint64_t)fi * a.nb) : (const void *)a.offsets,
+      (live && a.block_init) ? a.nb : 0u);
+  const uint32_t init = __builtin_amdgcn_raw_buffer_load_b8(ri, (int)b, 0, 0) & 0xFFu;
+  // table copy, unconditional 16-B loads issued behind the header (as the small kernel)
+  constexpr int kLutLoads = kLut14Bytes / 16 / (64 * kLpWaves);
+  static_assert(kLut14Bytes == kLutLoads * 16 * 64 * kLpWaves, "whole table per pass");
+  v4u32 L[kLutLoads];
+  {
+    const __amdgpu_buffer_rsrc_t rl =
+        uniform_rsrc(prepared + (l14 ? kLut14Off : 0), l14 ? (uint32_t)kLut14Bytes : (uint32_t)kLutBytes);
+#pragma unroll
+    for (int k = 0; k < kLutLoads; ++k)
+      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + 64u * kLpWaves * k) * 16u), 0, 0);
+  }
+  Tile t;
+  t.tile = tile;
+  t.f = fi;
+  t.b0 = b0;
+  t.valid = live && b < a.nb;
+  uint64_t fbytes = a.codes_bytes;
+  t.fbeg = 0;
+  if (a.frame_off) {
+    const uint64_t lo = ((uint64_t)__builtin_amdgcn_readlane(fo.y, 0) << 32) | __builtin_amdgcn_readlane(fo.x, 0);
+    const uint64_t hi = ((uint64_t)__builtin_amdgcn_readlane(fo.y, 1) << 32) | __builtin_amdgcn_readlane(fo.x, 1);
+    t.fbeg = lo;
+    fbytes = hi - lo;
+  }
+  t.fb32 = (uint32_t)(fbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : fbytes);
+  const uint32_t fbits = t.fb32 > 0x1FFFFFFFu ? 0xFFFFFFFFu : t.fb32 * 8u;
+  const bool exact_end = b + 1u < a.nb;
+  const uint32_t end_l = exact_end ? nxt : min(fbits, off + 64u * 16u);
+  const uint32_t last = live ? min(31u, a.nb - 1u - b0) : 0u;
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(off);
+  const uint32_t eb = __builtin_amdgcn_readlane(end_l, last);
+  t.start = (sb >> 3) & ~15u;
+  uint32_t endb = (eb >> 3) + 24u;
+  if (endb > t.fb32 + 16u) endb = t.fb32 + 16u;
+  t.span = endb > t.start ? min((endb - t.start + 15u) & ~15u, (uint32_t)kLpStageBytes) : 0u;
+  t.p = t.valid ? off - t.start * 8u : 0u;
+  t.init = init;
+  v4u32 R[kStageChunks];
+  span_issue(a, t, lane, R, live);
+  {
+    v4u32 *dst = reinterpret_cast<v4u32 *>(s_lp_lut);
+#pragma unroll
+    for (int k = 0; k < kLutLoads; ++k) dst[threadIdx.x + 64u * kLpWaves * k] = L[k];
+  }
+  __syncthreads();  // table in LDS
+  if (!live) return;  // wave-uniform; no barrier below
+  span_write(t, lane, R, stage);
+  wave_sync();
+  // output: descriptor at the tile's first block row (as out_tile, 32-block tiles)
+  const uint32_t bx = b % a.bw, by = b / a.bw;
+  const uint32_t by0 = __builtin_amdgcn_readfirstlane(b0 / a.bw);
+  const uint64_t base = (uint64_t)by0 * 8u * a.out_pitch;
+  const uint64_t rem = a.out_frame_bytes > base ? a.out_frame_bytes - base : 0u;
+  const __amdgpu_buffer_rsrc_t out = uniform_rsrc(a.out + (uint64_t)fi * a.out_frame_stride + base,
+                                                  (uint32_t)(rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull));
+  const uint32_t row0 = (by - by0) * 8u * (uint32_t)a.out_pitch + bx * 8u;
+  const uint32_t len = end_l - off;
+  const uint32_t mid = t.p + (len >> 1);
+  const uint32_t end = t.p + len;
+  const bool spec = t.valid && len >= 2u * (uint32_t)MH_LP_MIN_BITS && len <= 64u * 16u;
+  if (l14)
+    lp_decode<kDelta, kLut14Bits, false>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end, exact_end,
+                                         spec, init, out, row0, (uint32_t)a.out_pitch);
+  else
+    lp_decode<kDelta, kLutBits, true>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end, exact_end,
+                                      spec, init, out, row0, (uint32_t)a.out_pitch);
+}
+
 // Per-device launch parameters (CU count, batch-kernel occupancy per workgroup
 // size), computed once per device ordinal under std::call_once: no mutable state
 // is shared between devices or written by concurrent callers (the reference keeps
@@ -869,11 +1149,20 @@ const DeviceInfo *device_info(hipStream_t s) {
 }
 
 template <bool kDelta>
-int launch(const DecodeArgs &a0, hipStream_t s) {
+int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
   DecodeArgs a = a0;
   const DeviceInfo *di = device_info(s);
   if (!di) return MH_ERR_HIP;
   const int cus = di->cus;
+  if (lane_pairs && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
+    // experimental lane-pair decode (MH_FLAG_LANE_PAIRS): 32-block tiles
+    const uint32_t n_frames = a.total_tiles / a.tiles_per_frame;
+    a.tiles_per_frame = (a.nb + 31u) / 32u;
+    a.total_tiles = a.tiles_per_frame * n_frames;
+    a.n_groups = (a.total_tiles + kLpWaves - 1) / kLpWaves;
+    hipLaunchKernelGGL(mh_decode_lanepair_kernel<kDelta>, dim3(a.n_groups), dim3(kLpWaves * 64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
+  }
   if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // one tile per wave, kSmallWaves waves per workgroup: fewer workgroups copy the
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
@@ -937,7 +1226,7 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (!fr || !d_out || !fr->d_block_offsets || !fr->d_codes || !fr->d_table1 || !fr->d_table2)
     return MH_ERR_INVALID_ARG;
   if (fr->n_frames == 0 || (fr->n_frames > 1 && !fr->d_frame_code_offsets)) return MH_ERR_INVALID_ARG;
-  if (fr->flags & ~MH_FLAG_NO_DELTA) return MH_ERR_INVALID_ARG;
+  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_LANE_PAIRS)) return MH_ERR_INVALID_ARG;
   const mh_dims &d = fr->dims;
   if (!d.width || !d.height || d.width > MH_MAX_DIM || d.height > MH_MAX_DIM ||
       d.block_width != (d.width + 7) / 8 || d.block_height != (d.height + 7) / 8)
@@ -979,7 +1268,8 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (total > 0x7FFFFFFFull) return MH_ERR_CAPACITY;
   a.total_tiles = (uint32_t)total;
   hipStream_t s = (hipStream_t)stream;
-  return (fr->flags & MH_FLAG_NO_DELTA) ? launch<false>(a, s) : launch<true>(a, s);
+  const bool lp = (fr->flags & MH_FLAG_LANE_PAIRS) != 0;
+  return (fr->flags & MH_FLAG_NO_DELTA) ? launch<false>(a, s, lp) : launch<true>(a, s, lp);
 }
 
 }  // extern "C"

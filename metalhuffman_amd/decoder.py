@@ -168,8 +168,9 @@ def _frame_struct(frames: DeviceFrames, tables: DeviceTables) -> N.mh_frame:
 
 
 def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tensor] = None,
-           stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-    """Decode every frame into out[n, H, pitch] (pitch = W rounded up to 8)."""
+           stream: Optional[torch.cuda.Stream] = None, extra_flags: int = 0) -> torch.Tensor:
+    """Decode every frame into out[n, H, pitch] (pitch = W rounded up to 8).
+    extra_flags: decode-only flags ORed into the frame's (MH_FLAG_LANE_PAIRS)."""
     dev = frames.codes.device
     if tables.table1.device != dev:
         raise ValueError("tables and frames must live on the same device")
@@ -179,6 +180,7 @@ def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tenso
     if out.dtype != torch.uint8 or not out.is_contiguous() or out.shape[-2:] != (frames.height, pitch):
         raise ValueError(f"out must be contiguous uint8 [n, {frames.height}, {pitch}]")
     fr = _frame_struct(frames, tables)
+    fr.flags |= extra_flags
     N.check(N.lib().mh_decode(ctypes.byref(fr), out.data_ptr(), pitch, frames.height * pitch,
                               _stream_ptr(stream, dev)), "mh_decode")
     return out
