@@ -237,21 +237,6 @@ struct StepCfg {
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
   static constexpr uint32_t kMask = (2u << kBits) - 2u;       // byte address of a u16 entry
   static constexpr uint32_t kRefillAt = kCur - 32u;           // low byte <= this: sh >= 32
-  static constexpr bool kPair = false;
-};
-
-// The batch kernel's symbol-pair step (mh_lut.hpp kPairOff): u32 entries of the
-// 13-bit window, so the window's 13 bits go to bits 2..14 (kCur one lower).
-template <bool kEscapes, bool kMaskedRefill = true>
-struct PairCfg {
-  static constexpr bool kEsc = kEscapes;
-  static constexpr bool kSwz = false;
-  static constexpr bool kSpec = false;
-  static constexpr bool kMasked = kMaskedRefill;
-  static constexpr bool kPair = true;
-  static constexpr uint32_t kCur = 126u - (uint32_t)kLutBits;  // 113
-  static constexpr uint32_t kMask = (4u << kLutBits) - 4u;      // byte address of a u32 entry
-  static constexpr uint32_t kRefillAt = kCur - 32u;
 };
 
 using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  // the batch kernel's step
@@ -275,19 +260,10 @@ using Lut13Flat = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, 
 // entry's step word then advances sh and prev together (the low byte stays in
 // [kCur - 63, kCur], so it never borrows from prev).
 template <bool kDelta, class Cfg, class Src>
-__device__ __forceinline__ void decode_block_pair(const Src &src, const uint8_t *lut, uint32_t p,
-                                                  uint32_t prev, __amdgpu_buffer_rsrc_t out,
-                                                  uint32_t row0, uint32_t pitch, bool dead);
-
-template <bool kDelta, class Cfg, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut, uint32_t p,
                                              uint32_t prev, __amdgpu_buffer_rsrc_t out,
                                              uint32_t row0, uint32_t pitch, bool dead,
                                              uint32_t prio = 0) {
-  if constexpr (Cfg::kPair) {
-    decode_block_pair<kDelta, Cfg>(src, lut, p, prev, out, row0, pitch, dead);
-    return;
-  }
   const uint8_t *wa = src.at((p >> 5) * 4u);
   const auto rd = [&](const uint8_t *q) -> uint32_t {
     if constexpr (Cfg::kSwz)
@@ -406,90 +382,6 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
 #undef MH_LOOKUP
 #undef MH_FINISH
 #undef MH_REFILL_C
-}
-
-// One lane decodes one 8x8 block in 32 pair-steps of two symbols each
-// (AAPLShaders.metal:241-268 twice per table read). The pair table's entry for the
-// 13-bit window gives the state word after the first symbol (hi16) and after the
-// first two (lo16); when the two codes do not both fit the window (lo16 == hi16:
-// a long or escaped first code, or a second code cut off), the lanes concerned read
-// the entry of the window after the first symbol -- exec-masked, so the LDS sees
-// only those lanes -- and take its first symbol. Every pair-step yields exactly two
-// symbols, so the output schedule (4 states -> one output word, 8 bytes -> one row
-// store) is the single-step kernel's. Escapes (codes over 13 bits) take the second
-// level behind a wave-uniform ballot, as in decode_block.
-template <bool kDelta, class Cfg, class Src>
-__device__ __forceinline__ void decode_block_pair(const Src &src, const uint8_t *lut, uint32_t p,
-                                                  uint32_t prev, __amdgpu_buffer_rsrc_t out,
-                                                  uint32_t row0, uint32_t pitch, bool dead) {
-  const uint8_t *wa = src.at((p >> 5) * 4u);
-  uint32_t S = (prev << 8) + Cfg::kCur - (p & 31u);
-  uint32_t hi = word_at(wa);
-  uint32_t lo = word_at(wa + 4);
-  uint32_t nw = word_at(wa + 8);
-  const auto first = [&](uint32_t e, uint32_t s) -> uint32_t {
-    // escape (code over 13 bits) or invalid window: the second level
-    if constexpr (Cfg::kEsc) {
-      const bool esc = e < kEscapeBelow;
-      if (__builtin_expect(__ballot(esc) != 0, 0)) {
-        const uint64_t x = (((uint64_t)hi) << 32) | lo;
-        // the 3 window bits after the 13-bit index (which sits at bits 2..14)
-        const uint32_t x3 = (uint32_t)(x >> ((s - 1u) & 63u)) & 7u;
-        const uint32_t e2 = *reinterpret_cast<const uint16_t *>(
-            lut + kPairL2Off + 2u * (((e & 0xFFu) << kL2Bits) + x3));
-        e = esc ? e2 : e;
-      }
-    }
-    return e;
-  };
-#pragma unroll
-  for (uint32_t r = 0; r < 8; ++r) {
-    uint32_t sv[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      // keep sh < 32 at the start of every pair-step (two codes are <= 32 bits)
-      const bool c = (S & 0xFFu) <= Cfg::kRefillAt;
-      if (r || k) {
-        hi = c ? lo : hi;
-        lo = c ? nw : lo;
-        const uint32_t d = c ? 4u : 0u;
-        wa += d;
-        S += d * 8u;
-        if constexpr (!Cfg::kMasked) nw = word_at(wa + 8);
-      }
-      const uint64_t x = (((uint64_t)hi) << 32) | lo;
-      const uint32_t pe = *reinterpret_cast<const uint32_t *>(lut + ((uint32_t)(x >> (S & 63u)) & Cfg::kMask));
-      if constexpr (Cfg::kMasked) {
-        if ((r || k) && c) nw = word_at(wa + 8);
-      }
-      const uint32_t S0 = S;
-      const uint32_t Sa = S0 + first(pe >> 16, S0);
-      uint32_t Sb = S0 + (pe & 0xFFFFu);
-      const bool single = (pe >> 16) == (pe & 0xFFFFu);
-      if (__ballot(single)) {
-        if (single) {
-          const uint64_t x2 = (((uint64_t)hi) << 32) | lo;
-          const uint32_t pe2 =
-              *reinterpret_cast<const uint32_t *>(lut + ((uint32_t)(x2 >> (Sa & 63u)) & Cfg::kMask));
-          Sb = Sa + first(pe2 >> 16, Sa);
-        }
-      }
-      S = Sb;
-      if (kDelta) {
-        sv[2 * k] = Sa;
-        sv[2 * k + 1] = Sb;
-      } else {  // raw symbols: byte 1 of each step's own word
-        sv[2 * k] = Sa - S0 + 0xFFu;
-        sv[2 * k + 1] = Sb - Sa + 0xFFu;
-      }
-    }
-    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-    v2u32 v;
-    v.x = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
-    v.y = pack_prev4(sv[4], sv[5], sv[6], sv[7]);
-    const uint32_t off = dead ? 0xFFFFFFF0u : row0 + r * pitch;
-    __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
-  }
 }
 
 constexpr int kStageChunks = (kStageBytes / 16 + 63) / 64;  // 16-B chunks per lane (5)
@@ -708,15 +600,14 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
 // header of tile i+2 and the code span of tile i+1 are in flight into registers;
 // the span is written to the wave's LDS window once tile i has finished reading it.
 template <bool kDelta, class Cfg>
-__device__ __forceinline__ void batch_tiles(const DecodeArgs &a, uint8_t *tab, const uint8_t *gtab,
-                                            uint32_t gtab_bytes) {
+__device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   constexpr bool kSwz = Cfg::kSwz;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = blockDim.x >> 6;
   const uint32_t gstride = gridDim.x * nwaves;
   uint8_t *stage = s_stage + wave * kStageBytes;
-  const uint8_t *lut = tab;
+  const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
 #if MH_DIAG_STAMPS
   unsigned long long ts[kDiagSlots] = {};
   bool first_tile = true;
@@ -731,10 +622,10 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a, uint8_t *tab, c
   hdr_issue(a, t0, lane, hc);
 
   // ---- lookup table into LDS (shared by the workgroup) ----
-  if (gtab) {
-    const v4u32 *src = reinterpret_cast<const v4u32 *>(gtab);
-    v4u32 *dstv = reinterpret_cast<v4u32 *>(tab);
-    for (uint32_t i = threadIdx.x; i < gtab_bytes / 16u; i += blockDim.x) dstv[i] = src[i];
+  if (a.lut) {
+    const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
+    v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
   }
 
   v4u32 R[kStageChunks];
@@ -744,11 +635,10 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a, uint8_t *tab, c
   span_issue(a, cur, lane, R, cur_staged);
   hdr_issue(a, next_tile(t0), lane, hn);
 
-  if (gtab) {
+  if (a.lut) {
     __syncthreads();
   } else {
-    build_lut(a.t1, a.t2, a.t2_entries, reinterpret_cast<uint16_t *>(tab), &s_p0, threadIdx.x, blockDim.x,
-              [] { __syncthreads(); });
+    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
   MH_STAMP(2);
   if (cur_staged) span_write<kSwz>(cur, lane, R, stage);
@@ -830,40 +720,12 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
     mx = ml[0];
     mn = ml[1];
   }
-  uint8_t *tab = reinterpret_cast<uint8_t *>(s_lut);
-  const uint8_t *g = reinterpret_cast<const uint8_t *>(a.lut);
   if (MH_STAGE_SWIZZLE && a.lut && mx == mn)
-    batch_tiles<kDelta, Lut13Flat>(a, tab, g, kLutBytes);
+    batch_tiles<kDelta, Lut13Flat>(a);
   else if (MH_NOESC_PATH && a.lut && mx <= (uint32_t)kLutBits)
-    batch_tiles<kDelta, Lut13NoEsc>(a, tab, g, kLutBytes);
+    batch_tiles<kDelta, Lut13NoEsc>(a);
   else
-    batch_tiles<kDelta, Lut13>(a, tab, g, kLutBytes);
-}
-
-// The symbol-pair batch kernel (prepared tables only): the same persistent loop
-// with the pair step; flat tables (one code length: no two codes share a 13-bit
-// window unless they are <= 6 bits) keep the single step and swizzled stage. Its
-// LDS table (pair entries + second level, 34 KB) is shared by the flavours.
-#ifndef MH_PAIR_KERNEL          // 1: batch launches with a prepared table use the pair kernel
-#define MH_PAIR_KERNEL 1
-#endif
-#ifndef MH_PAIR_WAVES           // waves per workgroup of the pair kernel
-#define MH_PAIR_WAVES 8
-#endif
-static_assert(MH_PAIR_WAVES <= kMaxWavesPerWG, "the stage array holds kMaxWavesPerWG windows");
-__shared__ __attribute__((aligned(16))) uint8_t s_lut_pair[kPairBytes];
-
-template <bool kDelta>
-__global__ void __launch_bounds__(64 * MH_PAIR_WAVES) mh_decode_pair_kernel(const DecodeArgs a) {
-  const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
-  const uint32_t mx = ml[0], mn = ml[1];
-  const uint8_t *g = reinterpret_cast<const uint8_t *>(a.lut);
-  if (MH_STAGE_SWIZZLE && mx == mn)
-    batch_tiles<kDelta, Lut13Flat>(a, s_lut_pair, g, kLutBytes);
-  else if (MH_NOESC_PATH && mx <= (uint32_t)kLutBits)
-    batch_tiles<kDelta, PairCfg<false, MH_MASKED_REFILL != 0>>(a, s_lut_pair, g + kPairOff, kPairBytes);
-  else
-    batch_tiles<kDelta, PairCfg<true, MH_MASKED_REFILL != 0>>(a, s_lut_pair, g + kPairOff, kPairBytes);
+    batch_tiles<kDelta, Lut13>(a);
 }
 
 // ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------
@@ -1245,14 +1107,15 @@ struct DeviceInfo {
   std::once_flag once;
   int cus = 0;
   int occ[2][kMaxWavesPerWG + 1] = {};
-  int occ_pair[2] = {};  // pair kernel, MH_PAIR_WAVES per workgroup
 };
 DeviceInfo g_devinfo[kMaxDevices];
 
-template <class K>
-int occupancy_query(K kernel, int nw) {
+template <bool kDelta>
+int occupancy_query(int nw) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, nw * 64, 0) != hipSuccess || blocks < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mh_decode_kernel<kDelta>, nw * 64, 0) !=
+          hipSuccess ||
+      blocks < 1)
     blocks = 1;
   return blocks;
 }
@@ -1276,11 +1139,9 @@ const DeviceInfo *device_info(hipStream_t s) {
     const bool swap = hipGetDevice(&cur) == hipSuccess && cur != dev;
     if (swap && hipSetDevice(dev) != hipSuccess) return;
     for (int nw = 1; nw <= kMaxWavesPerWG; ++nw) {
-      d.occ[0][nw] = occupancy_query(mh_decode_kernel<false>, nw);
-      d.occ[1][nw] = occupancy_query(mh_decode_kernel<true>, nw);
+      d.occ[0][nw] = occupancy_query<false>(nw);
+      d.occ[1][nw] = occupancy_query<true>(nw);
     }
-    d.occ_pair[0] = occupancy_query(mh_decode_pair_kernel<false>, MH_PAIR_WAVES);
-    d.occ_pair[1] = occupancy_query(mh_decode_pair_kernel<true>, MH_PAIR_WAVES);
     if (swap) (void)hipSetDevice(cur);
     d.cus = prop.multiProcessorCount;  // last: nonzero marks the entry complete
   });
@@ -1308,14 +1169,6 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
     const uint32_t nw = kSmallWaves;
     a.n_groups = (a.total_tiles + nw - 1) / nw;
     hipLaunchKernelGGL(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), 0, s, a);
-    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
-  }
-  if (MH_PAIR_KERNEL && a.lut) {
-    const uint32_t nw = MH_PAIR_WAVES;
-    a.n_groups = (a.total_tiles + nw - 1) / nw;
-    const uint32_t resident = (uint32_t)(cus * di->occ_pair[kDelta ? 1 : 0]);
-    const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
-    hipLaunchKernelGGL(mh_decode_pair_kernel<kDelta>, dim3(grid), dim3(nw * 64), 0, s, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   // Waves per workgroup: spread a small launch (one 2048x1536 frame = 768 tiles)

@@ -23,18 +23,8 @@ constexpr int kLut14Entries = 1 << kLut14Bits;           // 16384 x u16
 constexpr int kLut14Off = kLutBytes;                     // byte offset in the buffer
 constexpr int kLut14Bytes = kLut14Entries * 2;           // 32768
 constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest, u32 shortest code length
-// ... and the batch kernel's symbol-pair table: for every 13-bit window a u32
-// [hi16: step word (or escape) of its first code | lo16: step word of the first
-// TWO codes when both lie inside the 13 bits, else the first one's again], then a
-// copy of the 13-bit table's second level (escapes of codes over 13 bits), so one
-// contiguous copy stages both in LDS.
-constexpr int kPairOff = kMaxLenOff + 16;                 // 51248
-constexpr int kPairEntries = kL1Entries;                  // 8192 x u32
-constexpr int kPairL2Off = kPairEntries * 4;              // 32768: L2 copy, relative to kPairOff
-constexpr int kPairBytes = kPairL2Off + (kLutEntries - kL1Entries) * 2;  // 34848
-constexpr int kPreparedBytes = kPairOff + kPairBytes;     // 86096
-static_assert(kLutBytes % 16 == 0 && kLut14Bytes % 16 == 0 && kPairBytes % 16 == 0,
-              "lut copies use 16-byte chunks");
+constexpr int kPreparedBytes = kMaxLenOff + 16;          // 51248
+static_assert(kLutBytes % 16 == 0 && kLut14Bytes % 16 == 0, "lut copy uses 16-byte chunks");
 static_assert(kL2Subtables < 240, "escape entries must stay below the smallest step word");
 
 // LUT entry format ("step word"): a valid {symbol, bitWidth} becomes
@@ -50,23 +40,6 @@ __device__ __forceinline__ uint32_t step_word(uint32_t e) {
   return len ? (((e & 0xFFu) << 8) - len) & 0xFFFFu : 0u;
 }
 constexpr uint32_t kEscapeBelow = 240u;
-
-// Pair-table entry of 13-bit window p whose 13-bit table value is w1 (a step word,
-// an escape, or 0 for an invalid window); lookup(pat16) returns the split tables'
-// {symbol | bitWidth << 8} for a 16-bit pattern. The second code is read from the
-// window's remaining bits with zeros after them: a prefix code whose length fits
-// the known bits is exactly that code (HuffmanUtil.cpp:961-995's rule on the
-// shifted window), anything longer leaves the entry single.
-template <class Lookup>
-__device__ __forceinline__ uint32_t pair_entry(uint32_t p, uint32_t w1, Lookup lookup) {
-  if (w1 < kEscapeBelow) return w1 | (w1 << 16);
-  const uint32_t len1 = (256u - (w1 & 0xFFu)) & 0xFFu;
-  if (len1 >= (uint32_t)kLutBits) return w1 | (w1 << 16);
-  const uint32_t e2 = lookup(((p << len1) & (uint32_t)(kL1Entries - 1)) << kL2Bits);
-  const uint32_t len2 = e2 >> 8;
-  if (len2 == 0 || len2 > (uint32_t)kLutBits - len1) return w1 | (w1 << 16);
-  return (w1 << 16) | ((w1 + step_word(e2)) & 0xFFFFu);
-}
 
 // split_lookup for kBatch windows at once, T1 from LDS: every T2 read is issued
 // before any is used (one L2 round trip per batch instead of one per window).
@@ -157,31 +130,10 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     lut[p] = (uint16_t)(sub < (uint32_t)kL2Subtables ? sub : 0u);
   }
   const uint32_t nl2 = ((uint32_t)kL1Entries - P0) << kL2Bits;
-  uint16_t *pl2 = reinterpret_cast<uint16_t *>(buf + kPairOff + kPairL2Off);
-  for (uint32_t i = tid; i < (uint32_t)(kLutEntries - kL1Entries); i += nt) pl2[i] = 0;
   for (uint32_t i = tid; i < nl2 && i < (uint32_t)(kL2Entries - (1 << kL2Bits)); i += nt) {
     uint32_t pat[1] = {(P0 << kL2Bits) + i}, e[1];
     split_lookup_batch(s_t1, t2, t2_entries, pat, e);
     lut[kL1Entries + (1 << kL2Bits) + i] = (uint16_t)step_word(e[0]);
-    pl2[(1 << kL2Bits) + i] = (uint16_t)step_word(e[0]);
-  }
-  // the symbol-pair table (batch kernel): first code's word as the 13-bit table has it
-  uint32_t *pair = reinterpret_cast<uint32_t *>(buf + kPairOff);
-  for (uint32_t p = tid; p < (uint32_t)kL1Entries; p += nt) {
-    uint32_t w1;
-    if (p >= P0) {
-      const uint32_t sub = p - P0 + 1;
-      w1 = sub < (uint32_t)kL2Subtables ? sub : 0u;
-    } else {
-      uint32_t pat[1] = {p << kL2Bits}, e[1];
-      split_lookup_batch(s_t1, t2, t2_entries, pat, e);
-      w1 = step_word(e[0]);
-    }
-    pair[p] = pair_entry(p, w1, [&](uint32_t pat16) {
-      uint32_t pt[1] = {pat16}, e[1];
-      split_lookup_batch(s_t1, t2, t2_entries, pt, e);
-      return e[0];
-    });
   }
   // [longest code, shortest code, 0, 0]
   if (tid < 4)

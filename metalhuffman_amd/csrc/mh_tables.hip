@@ -193,42 +193,36 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
                                      : (uint32_t)kL1Entries;
   const uint32_t nl2 = ((uint32_t)kL1Entries - P0) << kL2Bits;
   constexpr uint32_t kL2Region = (uint32_t)(kLutEntries - kL1Entries);
-  constexpr uint32_t kAll = (uint32_t)kL1Entries + kL2Region + (uint32_t)kLut14Entries + (uint32_t)kPairEntries;
+  constexpr uint32_t kAll = (uint32_t)kL1Entries + kL2Region + (uint32_t)kLut14Entries;
   const uint32_t per = (kAll + gridDim.x - 1) / gridDim.x;
   const uint32_t lo = blockIdx.x * per, hi = min(kAll, lo + per);
   uint16_t *out = reinterpret_cast<uint16_t *>(lut);
   uint16_t *out14 = reinterpret_cast<uint16_t *>(lut + kLut14Off);
-  uint32_t *outp = reinterpret_cast<uint32_t *>(lut + kPairOff);
-  uint16_t *outp2 = reinterpret_cast<uint16_t *>(lut + kPairOff + kPairL2Off);
   auto lookup = [&](uint32_t pat16) -> uint32_t {
     uint32_t e = s_t1[pat16 >> 8];
     if ((e >> 8) == 0) e = s_t2[(e & 0xFFu) * 256u + (pat16 & 0xFFu)];
     return e;
   };
-  const auto l1_word = [&](uint32_t p) -> uint32_t {
-    if (p >= P0) {
-      const uint32_t sub = p - P0 + 1;
-      return sub < (uint32_t)kL2Subtables ? sub : 0u;
-    }
-    return step_word(lookup(p << kL2Bits));
-  };
   for (uint32_t v = lo + tid; v < hi; v += blockDim.x) {
     if (v < (uint32_t)kL1Entries) {
-      out[v] = (uint16_t)l1_word(v);
+      const uint32_t p = v;
+      uint32_t w;
+      if (p >= P0) {
+        const uint32_t sub = p - P0 + 1;
+        w = sub < (uint32_t)kL2Subtables ? sub : 0u;
+      } else {
+        w = step_word(lookup(p << kL2Bits));
+      }
+      out[p] = (uint16_t)w;
     } else if (v < (uint32_t)kL1Entries + kL2Region) {
       const uint32_t i = v - (uint32_t)kL1Entries;  // L2 subtable 0 and the padding stay zero
       const uint32_t j = i - (1u << kL2Bits);
       const bool live = i >= (1u << kL2Bits) && j < nl2 && j < (uint32_t)(kL2Entries - (1 << kL2Bits));
-      const uint16_t w = (uint16_t)(live ? step_word(lookup((P0 << kL2Bits) + j)) : 0u);
-      out[kL1Entries + i] = w;
-      outp2[i] = w;  // the pair table's copy of the second level
-    } else if (v < (uint32_t)kL1Entries + kL2Region + (uint32_t)kLut14Entries) {
+      out[kL1Entries + i] = (uint16_t)(live ? step_word(lookup((P0 << kL2Bits) + j)) : 0u);
+    } else {
       const uint32_t q = v - (uint32_t)kL1Entries - kL2Region;
       const uint32_t e = lookup(q << (16 - kLut14Bits));
       out14[q] = (uint16_t)((e >> 8) <= (uint32_t)kLut14Bits ? step_word(e) : 0u);
-    } else {
-      const uint32_t p = v - (uint32_t)kL1Entries - kL2Region - (uint32_t)kLut14Entries;
-      outp[p] = pair_entry(p, l1_word(p), lookup);
     }
   }
   __syncthreads();
