@@ -13,7 +13,7 @@ cat gpurun_out/bench.json
 : > gpurun_out/ktrace_summary.txt
 # same steps / warm-up as the bench line each number is compared with (the frame
 # headline: 200 / 20; the extras: bench.py's own counts)
-for spec in frame:200:20 batch:256:256 tile8192:512:512 tile8192_random:512:512; do
+for spec in frame:20:5 batch:256:256 tile8192:512:512 tile8192_random:512:512; do
   IFS=: read wl k w <<< "$spec"
   rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_$wl
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --steps $k --warmup $w --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }

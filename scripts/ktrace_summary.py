@@ -4,8 +4,10 @@ Grouped by kernel and launch shape; compare with the bench line's
 roofline.kernel_us_avg of the same command (scripts/gpu_check.sh profiles one
 workload per command). Counts include warm-up, the untimed first graph replay,
 the timed graph replay and the eager per-launch pass (bench.Workload.run), all
-the same launch. `timed_avg` is the mean over the timed replay alone: launches
-[n - 2K, n - K) in start order, K = --steps of the profiled command (default 200).
+the same launch. `timed_avg` is the mean over the timed replay alone, K = --steps of
+the profiled command (default 200): the K decode launches that follow the last
+launch-gate kernel (bench.py's gated region, scripts/micro/launch_gate.hip), or, in a
+trace without the gate, launches [n - 2K, n - K) in start order.
 
     python scripts/ktrace_summary.py gpurun_out/prof_frame [K]
 """
@@ -18,8 +20,11 @@ import sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 groups = collections.defaultdict(list)
+gates = []
 for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
+        if "gate_kernel" in r["Kernel_Name"]:
+            gates.append(int(r["Start_Timestamp"]))
         if "mh_decode" not in r["Kernel_Name"]:
             continue
         key = (r["Kernel_Name"].split("mh_decode")[1].split("_kernel")[0] or "batch", int(r["Grid_Size_X"]),
@@ -32,7 +37,11 @@ for (k, g, w, lds, v), d in sorted(groups.items(), key=lambda kv: -len(kv[1])):
     d.sort()
     dur = [x for _, x in d]
     n = len(dur)
-    timed = dur[n - 2 * steps: n - steps] if n >= 2 * steps else []
+    if gates:
+        after = [x for t, x in d if t > max(gates)]
+        timed = after[:steps] if len(after) >= steps else []
+    else:
+        timed = dur[n - 2 * steps: n - steps] if n >= 2 * steps else []
     ta = f"{statistics.mean(timed):9.3f}" if timed else f"{'-':>9}"
     print(f"{k:>8} {g:12d} {w:5d} {lds:6d} {v:5d} {n:5d} {statistics.mean(dur):9.3f} "
           f"{statistics.median(dur):9.3f} {min(dur):8.3f} {ta}")
