@@ -305,6 +305,12 @@ class _Gate:
         return True
 
     def arm(self, stream: int) -> None:
+        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "wait":  # A/B: stream wait on the flag
+            import ctypes
+            self.lib.gate_arm_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            if self.lib.gate_arm_wait(self.h, self.d, stream) != 0:
+                raise RuntimeError("launch gate: stream wait failed")
+            return
         if self.lib.gate_arm(self.h, self.d, stream, 200_000) != 0:  # opens by itself after 200 ms
             raise RuntimeError("launch gate: kernel launch failed")
 

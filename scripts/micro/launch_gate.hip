@@ -50,6 +50,16 @@ int gate_arm(unsigned *host_ptr, const unsigned *dev_ptr, void *stream, unsigned
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The same gate as a stream wait on the flag (hipStreamWaitValue32: the command
+// processor itself waits for the value; no kernel). A/B against the polling kernel.
+int gate_arm_wait(unsigned *host_ptr, const unsigned *dev_ptr, void *stream) {
+  __atomic_store_n(host_ptr, 0u, __ATOMIC_SEQ_CST);
+  return hipStreamWaitValue32((hipStream_t)stream, const_cast<unsigned *>(dev_ptr), 1u, hipStreamWaitValueGte,
+                              0xFFFFFFFFu) == hipSuccess
+             ? 0
+             : -1;
+}
+
 void gate_open(unsigned *host_ptr) { __atomic_store_n(host_ptr, 1u, __ATOMIC_SEQ_CST); }
 
 void gate_destroy(unsigned *host_ptr) { (void)hipHostFree(host_ptr); }
