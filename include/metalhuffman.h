@@ -186,7 +186,12 @@ size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height);
  * header's content is unspecified.
  * d_workspace: 256-byte aligned, mh_encode_workspace_bytes(). The return value
  * covers only argument checks and launch errors. A frame encoded this way goes to
- * mh_build_tables_device (the header) and mh_decode without touching the host. */
+ * mh_build_tables_device (the header) and mh_decode without touching the host.
+ * Every call leaves the workspace's symbol histogram zeroed; a caller that
+ * zero-filled the workspace once before its first use may pass
+ * MH_ENCODE_WORKSPACE_ZEROED in `flags` to skip the per-call clear (one memset
+ * launch, ~2 us of a ~33 us frame). */
+#define MH_ENCODE_WORKSPACE_ZEROED 0x100u
 int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t height, uint32_t flags,
                                  uint8_t *d_canon_header, uint8_t *d_codes, uint64_t codes_cap,
                                  uint64_t *d_codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,

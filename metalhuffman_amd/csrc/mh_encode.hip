@@ -155,6 +155,42 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
 }
 
+#ifndef MH_TREE_BITONIC  // 1: each merge round orders the queue heads by a register bitonic merge
+#define MH_TREE_BITONIC 1
+#endif
+
+// Value of lane (lane ^ D) (64-lane wave): permlane32_swap for 32, ds_swizzle's xor
+// mode for 16 and 4, DPP (row rotate by 8, quad permutes) for 8, 2, 1.
+template <uint32_t D>
+__device__ __forceinline__ uint32_t xor_partner(uint32_t lane, uint32_t v) {
+  if constexpr (D == 32 || D == 16) {
+    // the swap leaves lane ^ D's value in the first result for the upper lane of
+    // each pair, in the second for the lower
+    const auto r = D == 32 ? __builtin_amdgcn_permlane32_swap(v, v, false, false)
+                           : __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & D) ? r[0] : r[1];
+  } else if constexpr (D == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128 /* row_ror:8 */, 0xF, 0xF, true);
+  } else if constexpr (D == 4) {  // row_half_mirror (i -> 7 - i) then reverse within quads
+    const int m = __builtin_amdgcn_mov_dpp((int)v, 0x141 /* row_half_mirror */, 0xF, 0xF, true);
+    return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x1B /* quad_perm [3,2,1,0] */, 0xF, 0xF, true);
+  } else if constexpr (D == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E /* quad_perm [2,3,0,1] */, 0xF, 0xF, true);
+  } else {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, true);
+  }
+}
+
+// One half-cleaner stage of an ascending bitonic sort over the wave: the lower lane
+// of each (lane, lane ^ D) pair keeps the smaller key, the upper the larger.
+template <uint32_t D>
+__device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
+  const uint64_t p = ((uint64_t)xor_partner<D>(lane, (uint32_t)(key >> 32)) << 32) |
+                     xor_partner<D>(lane, (uint32_t)key);
+  const bool take = (p < key) != ((lane & D) != 0u);  // keys are distinct
+  key = take ? p : key;
+}
+
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
 // from the 256 counts. The reference keeps every node in one array sorted by weight,
 // inserts at upper_bound (a new node goes after all nodes of equal weight) and merges
@@ -168,7 +204,9 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
 // the canonical codes
 // (huff_util.hpp:94-193), the code table, the code byte count and the status
 // (mh_code_lengths' errors, the caller's capacity).
-__global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uint8_t *canon_out,
+constexpr uint32_t kTreeThreads = 1024;  // 4 per symbol in the ranking; 256 (one per symbol) elsewhere
+
+__global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, uint8_t *canon_out,
                                                        uint32_t *table, uint64_t *meta, uint64_t *codes_len_out,
                                                        uint64_t codes_cap, int32_t *status) {
   constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
@@ -179,18 +217,28 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
 #else
 #define MH_TREE_STAMP(k)
 #endif
-  __shared__ uint32_t s_lw[384], s_iw[384], s_qv[64], s_qid[64];  // queues padded with kEnd
+  __shared__ uint32_t s_lw[384], s_iw[384];  // queues padded with kEnd
+#if !MH_TREE_BITONIC
+  __shared__ uint32_t s_qv[64], s_qid[64];
+#endif
   __shared__ __attribute__((aligned(16))) uint64_t s_key[256];
   __shared__ uint32_t s_leaf_sym[256], s_len[256], s_par[2][512], s_dep[2][512];
   __shared__ uint32_t s_wcnt[4][17], s_first[17], s_n, s_bad;
+  __shared__ uint32_t s_below[4][256];
   __shared__ unsigned long long s_total;
   const uint32_t tid = threadIdx.x;
+  const bool sym_thread = tid < 256u;  // thread tid < 256 owns symbol tid
   uint64_t f = 0;
+  if (sym_thread) {
 #pragma unroll
-  for (uint32_t k = 0; k < kHistParts; ++k) f += hist[k * 256 + tid];
-  s_len[tid] = 0;
-  s_lw[tid] = kEnd;
-  s_iw[tid] = kEnd;
+    for (uint32_t k = 0; k < kHistParts; ++k) f += hist[k * 256 + tid];
+    // leave the histogram zeroed for the next frame's split (MH_ENCODE_WORKSPACE_ZEROED)
+#pragma unroll
+    for (uint32_t k = 0; k < kHistParts; ++k) hist[k * 256 + tid] = 0;
+    s_len[tid] = 0;
+    s_lw[tid] = kEnd;
+    s_iw[tid] = kEnd;
+  }
   if (tid < 128) s_lw[256 + tid] = s_iw[256 + tid] = kEnd;
   if (tid == 0) {
     s_n = 0;
@@ -203,19 +251,24 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
     // rank of this leaf in (weight, symbol) order: count the smaller keys among all
     // 256 (16-byte broadcast reads, one 64-bit compare per key). Absent symbols
     // have key 0, below every present one: subtract their count afterwards.
-    const uint64_t key = f ? (f << 8) | tid : 0;
-    s_key[tid] = key;
+    // Four threads per symbol, a quarter of the keys each (the compares are VALU
+    // issue-bound: one wave per SIMD took 6 K clocks for all 256).
+    if (sym_thread) s_key[tid] = f ? (f << 8) | tid : 0;
     const uint32_t present = (uint32_t)__syncthreads_count(f != 0);
+    const uint32_t ks = tid & 255u, part = tid >> 8;
+    const uint64_t key = s_key[ks];
     uint32_t below = 0;
-    const ulonglong2 *kv = reinterpret_cast<const ulonglong2 *>(s_key);
+    const ulonglong2 *kv = reinterpret_cast<const ulonglong2 *>(s_key) + part * 32u;
 #pragma unroll 16
-    for (uint32_t t = 0; t < 128; ++t) {  // same address across the wave: broadcast reads
+    for (uint32_t t = 0; t < 32; ++t) {  // same address across the wave: broadcast reads
       const ulonglong2 v = kv[t];
       below += v.x < key ? 1u : 0u;
       below += v.y < key ? 1u : 0u;
     }
-    if (f) {
-      const uint32_t rank = below - (256u - present);
+    s_below[part][ks] = below;
+    __syncthreads();
+    if (sym_thread && f) {
+      const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
       s_leaf_sym[rank] = tid;
       s_lw[rank] = (uint32_t)f;
     }
@@ -241,6 +294,27 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
     const uint32_t lane = tid;
     uint32_t li = 0, ii = 0, ni = 0, m = 0;
     while (m + 1 < n) {
+#if MH_TREE_BITONIC
+      // Q[0..63] by a bitonic merge in registers: key = weight : type : queue
+      // position (a leaf sorts before an internal node of equal weight; each queue
+      // keeps its order). min(A[i], B[63 - i]) holds the 64 smallest of both heads as
+      // a bitonic sequence; six half-cleaner stages (partners from permlane32_swap,
+      // ds_swizzle and DPP -- no LDS round trip) sort it.
+      uint64_t key;
+      {
+        const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + 63u - lane];
+        const bool a = lv <= iv;  // equal weight: the leaf (type 0) first
+        key = ((uint64_t)(a ? lv : iv) << 32) | (a ? li + lane : (0x10000u | (ii + 63u - lane)));
+      }
+      bitonic_stage<32>(lane, key);
+      bitonic_stage<16>(lane, key);
+      bitonic_stage<8>(lane, key);
+      bitonic_stage<4>(lane, key);
+      bitonic_stage<2>(lane, key);
+      bitonic_stage<1>(lane, key);
+      const uint32_t q = (uint32_t)(key >> 32), kl = (uint32_t)key;
+      const uint32_t qid = (kl & 0x10000u) ? n + (kl & 0xFFFFu) : kl;
+#else
       const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + lane];
       uint32_t rl = 0, ri = 0;  // internal candidates < lv; leaf candidates <= iv
 #pragma unroll
@@ -259,10 +333,20 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
       }
       __builtin_amdgcn_wave_barrier();
       const uint32_t q = s_qv[lane], qid = s_qid[lane];
+#endif
       const uint32_t s0 = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_readlane(q, 1);
       uint32_t k = (uint32_t)__popcll(__ballot((lane & 1u) && q <= s0));  // Q sorted: a prefix
       k = min(k, n - 1 - m);
       const uint32_t nl = (uint32_t)__popcll(__ballot(lane < 2 * k && qid < n));
+#if MH_TREE_BITONIC
+      // pair j = lanes (2j, 2j+1): the odd lane adds its even neighbour (DPP) and
+      // appends the new node; both lanes point their node at it
+      const uint32_t qe = xor_partner<1>(lane, q);
+      if (lane < 2 * k) {
+        if (lane & 1u) s_iw[ni + (lane >> 1)] = qe + q;
+        s_par[0][qid] = n + ni + (lane >> 1);
+      }
+#else
       const uint32_t qa = __shfl(q, 2 * lane), qb = __shfl(q, 2 * lane + 1);
       const uint32_t ia = __shfl(qid, 2 * lane), ib = __shfl(qid, 2 * lane + 1);
       if (lane < k) {
@@ -270,6 +354,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
         s_par[0][ia] = n + ni + lane;
         s_par[0][ib] = n + ni + lane;
       }
+#endif
       __builtin_amdgcn_wave_barrier();
       li += nl;
       ii += 2 * k - nl;
@@ -280,7 +365,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   __syncthreads();
   MH_TREE_STAMP(3);
   // depths by pointer jumping: dep = 1 + dep(parent) over parent links, root 0
-  for (uint32_t i = tid; i < nodes; i += 256) {
+  for (uint32_t i = tid; i < nodes; i += kTreeThreads) {
     s_dep[0][i] = i == root ? 0u : 1u;
     if (i == root) s_par[0][i] = root;
   }
@@ -290,7 +375,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   // at least 32 deep, above the 16-bit limit either way (MH_ERR_CODE_TOO_LONG)
   uint32_t cur = 0;
   for (uint32_t step = 0; step < 5; ++step) {
-    for (uint32_t i = tid; i < nodes; i += 256) {
+    for (uint32_t i = tid; i < nodes; i += kTreeThreads) {
       const uint32_t p = s_par[cur][i];
       s_dep[cur ^ 1][i] = s_dep[cur][i] + s_dep[cur][p];
       s_par[cur ^ 1][i] = s_par[cur][p];
@@ -309,8 +394,8 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   }
   __syncthreads();
   MH_TREE_STAMP(5);
-  const uint32_t L = s_len[tid];
-  canon_out[tid] = (uint8_t)L;
+  const uint32_t L = sym_thread ? s_len[tid] : 0u;  // 0 matches no length below
+  if (sym_thread) canon_out[tid] = (uint8_t)L;
   // codes per length and each symbol's rank among equal lengths (symbol order):
   // one ballot per length per wave, per-wave counts through LDS
   const uint32_t wave = tid >> 6, lane = tid & 63u;
@@ -319,11 +404,11 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
   for (uint32_t l = 1; l <= 16; ++l) {
     const uint64_t m = __ballot(L == l);
     if (L == l) in_wave = (uint32_t)__popcll(m & below);
-    if (lane == 0) s_wcnt[wave][l] = (uint32_t)__popcll(m);
+    if (lane == 0 && wave < 4u) s_wcnt[wave][l] = (uint32_t)__popcll(m);
   }
   uint64_t bits = f * L;  // sum of count x length: wave reduction, one LDS atomic per wave
   for (int o = 32; o; o >>= 1) bits += __shfl_xor(bits, o);
-  if (lane == 0) atomicAdd(&s_total, (unsigned long long)bits);
+  if (lane == 0 && wave < 4u) atomicAdd(&s_total, (unsigned long long)bits);
   __syncthreads();
   MH_TREE_STAMP(6);
   if (tid < 64) {
@@ -349,7 +434,7 @@ __global__ void __launch_bounds__(256) enc_tree_kernel(const uint64_t *hist, uin
     for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
     e = ((((s_first[L] + rank) << (16 - L)) & 0xFFFFu) << 16) | L;
   }
-  table[tid] = e;
+  if (sym_thread) table[tid] = e;
   if (tid == 0) {
     const uint64_t total = s_total;
     const uint64_t len = (total + 7) / 8 + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
@@ -559,7 +644,7 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
                                  int32_t *d_status, void *d_workspace, size_t workspace_bytes, void *stream) {
   if (!d_gray || !d_canon_header || !d_codes || !d_block_offsets || !d_workspace)
     return MH_ERR_INVALID_ARG;
-  if (flags & ~MH_FLAG_NO_DELTA) return MH_ERR_INVALID_ARG;
+  if (flags & ~(MH_FLAG_NO_DELTA | MH_ENCODE_WORKSPACE_ZEROED)) return MH_ERR_INVALID_ARG;
   if (!width || !height || width > MH_MAX_DIM || height > MH_MAX_DIM) return MH_ERR_DIMS;
   if (((uintptr_t)d_codes & 3u) || ((uintptr_t)d_workspace & 255u)) return MH_ERR_ALIGN;
   const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
@@ -572,12 +657,15 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const uint64_t ntiles = (nb + kScanTile - 1) / kScanTile;
   if (g256 == 0 || ntiles > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
 
-  if (hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess) return MH_ERR_HIP;
+  // the tree kernel zeroes the histogram after reading it, for the next call
+  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) && hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess)
+    return MH_ERR_HIP;
+  flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
   const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, MH_SPLIT_WGS);
   hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
                      w.sym, d_block_init, w.hist);
-  hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(256), 0, s, w.hist, d_canon_header, w.table, w.meta,
+  hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
                      d_codes_len, codes_cap, d_status);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
                      w.tsum, w.meta, reinterpret_cast<uint32_t *>(d_codes));

@@ -52,7 +52,9 @@ class Encoder:
         bw, bh = block_grid(width, height)
         self.nb = bw * bh
         ws = int(N.lib().mh_encode_workspace_bytes(width, height))
-        self.workspace = torch.empty(ws + 256, dtype=torch.uint8, device=self.device)
+        # zero-filled once: every encode leaves the histogram zeroed for the next, so
+        # the calls pass MH_ENCODE_WORKSPACE_ZEROED and skip the per-call clear
+        self.workspace = torch.zeros(ws + 256, dtype=torch.uint8, device=self.device)
         self.cap = (self.nb * 64 * 2 + N.MH_CODES_PAD + 3) // 4 * 4 + 16
 
     def encode(self, gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False,
@@ -68,7 +70,7 @@ class Encoder:
         base = self.workspace.data_ptr()
         aligned = (base + 255) // 256 * 256
         N.check(N.lib().mh_encode_frame_device(
-            gray.data_ptr(), self.width, self.height, flags,
+            gray.data_ptr(), self.width, self.height, flags | N.MH_ENCODE_WORKSPACE_ZEROED,
             canon.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), codes.data_ptr(), self.cap,
             ctypes.byref(n), offs.data_ptr(), init.data_ptr() if init is not None else None,
             aligned, self.workspace.numel() - (aligned - base), _stream_ptr(stream, self.device)),
@@ -100,7 +102,8 @@ class Encoder:
         base = self.workspace.data_ptr()
         aligned = (base + 255) // 256 * 256
         N.check(N.lib().mh_encode_frame_device_async(
-            gray.data_ptr(), self.width, self.height, flags, canon.data_ptr(), codes.data_ptr(),
+            gray.data_ptr(), self.width, self.height, flags | N.MH_ENCODE_WORKSPACE_ZEROED,
+            canon.data_ptr(), codes.data_ptr(),
             codes.numel(), meta.data_ptr(), offs.data_ptr(), init.data_ptr() if init is not None else None,
             meta.data_ptr() + 8, aligned, self.workspace.numel() - (aligned - base),
             _stream_ptr(stream, self.device)), "mh_encode_frame_device_async")

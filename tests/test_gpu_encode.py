@@ -232,3 +232,46 @@ def test_device_encoder_matches_reference_encoder_hashes(mh, device, bigbridge, 
     assert codes.size == rec["huffbuff_bytes"]
     assert sha(codes) == rec["huffbuff_sha256"]
     assert sha(dev.block_offsets.cpu().numpy().view(np.uint32).astype("<u4")) == rec["offsets_sha256"]
+
+
+def test_async_encode_workspace_flag(mh, device, bigbridge):
+    """Without MH_ENCODE_WORKSPACE_ZEROED the call clears the histogram itself (a
+    workspace full of garbage still encodes exactly); with it, a workspace that was
+    zero-filled once stays valid call after call (each tree kernel re-zeroes the
+    histogram it consumed), including after a rejected frame."""
+    import ctypes
+    import torch
+    from metalhuffman_amd import _native as N
+    from metalhuffman_amd.encoder import Encoder
+    from metalhuffman_amd import frames as F
+    h, w = 512, 768
+    img = np.ascontiguousarray(F.block_shuffle(bigbridge, 40)[:h, :w])
+    ref = mh.encode_frame(img)
+    enc = Encoder(w, h, device)
+    d = torch.from_numpy(img).to(device)
+    enc.workspace.fill_(0xFF)
+    codes = torch.empty(enc.cap, dtype=torch.uint8, device=device)
+    offs = torch.empty(enc.nb, dtype=torch.int32, device=device)
+    canon = torch.empty(256, dtype=torch.uint8, device=device)
+    meta = torch.zeros(2, dtype=torch.int64, device=device)
+    base = enc.workspace.data_ptr()
+    aligned = (base + 255) // 256 * 256
+    N.check(N.lib().mh_encode_frame_device_async(
+        d.data_ptr(), w, h, 0, canon.data_ptr(), codes.data_ptr(), codes.numel(), meta.data_ptr(),
+        offs.data_ptr(), None, meta.data_ptr() + 8, aligned, enc.workspace.numel() - (aligned - base),
+        ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)), "mh_encode_frame_device_async")
+    torch.cuda.synchronize(device)
+    n = int(meta[0].item())
+    assert np.array_equal(canon.cpu().numpy(), ref.canon)
+    assert np.array_equal(codes[:n].cpu().numpy(), ref.codes)
+    # the flag path (Encoder): zero-filled once, then frames, a rejected one, frames
+    enc2 = Encoder(w, h, device)
+    bad = torch.from_numpy(image_from_block_deltas(fibonacci_deltas(18, h * w, seed=2), w, h)).to(device)
+    for k, g in enumerate([d, bad, d, d]):
+        a = enc2.encode_async(g)
+        torch.cuda.synchronize(device)
+        if k == 1:
+            assert int(a.status.item()) == -3
+            continue
+        r = a.result()
+        assert np.array_equal(r.canon, ref.canon) and np.array_equal(r.codes.cpu().numpy(), ref.codes), k
