@@ -155,6 +155,9 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
 }
 
+#ifndef MH_SCAN_TICKET   // 1: the scan's last workgroup (completion ticket) scans the tile totals;
+#define MH_SCAN_TICKET 0   // 0: each packing workgroup sums the totals before its own tile
+#endif
 #ifndef MH_TREE_BITONIC  // 1: each merge round orders the queue heads by a register bitonic merge
 #define MH_TREE_BITONIC 1
 #endif
@@ -512,6 +515,12 @@ __global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym,
   uint32_t total;
   const uint32_t pre = wg_exclusive_scan(x, s_w, &total);
   if (i < nb) bpre[i] = pre;
+#if !MH_SCAN_TICKET
+  // tile totals only: each packing workgroup sums the totals before its tile
+  if (tid == 0) tsum[blockIdx.x] = total;
+  (void)last;
+  return;
+#endif
   if (tid == 0) {
     // The tile total goes out as a device-scope store (written through past this
     // XCD's L2) and is acknowledged before the ticket is taken, so the last
@@ -563,6 +572,8 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
   tab[tid] = table[tid];
   const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlocks, b = b0 + (tid >> 3);
   const bool on = b < nb;
+  const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
+#if MH_SCAN_TICKET
   const uint32_t o = on ? blen_prefix[b] + toff[b / kScanTile] : 0u;
   if (on && part == 0) offsets[b] = o;
   if (tid == 0) {
@@ -570,8 +581,31 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
     s_start = o;
     s_end = bn < nb ? blen_prefix[bn] + toff[bn / kScanTile] : (uint32_t)meta[kTotalBits];
   }
-  const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
   __syncthreads();
+#else
+  // this workgroup's tile offset: wave 0 sums the scan's tile totals before it
+  // (<= a few hundred L2-resident words) -- no completion ticket in the scan
+  __shared__ uint32_t s_toff[2];
+  const uint32_t t = (uint32_t)(b0 / kScanTile);
+  if (tid < 64) {
+    uint32_t acc = 0;
+    for (uint32_t i = tid; i < t; i += 64) acc += toff[i];
+    for (uint32_t d = 32; d; d >>= 1) acc += __shfl_xor(acc, d);
+    if (tid == 0) {
+      s_toff[0] = acc;
+      s_toff[1] = acc + toff[t];  // the next tile's offset (read only if this tile ends here)
+    }
+  }
+  __syncthreads();
+  const uint32_t o = on ? blen_prefix[b] + s_toff[0] : 0u;
+  if (on && part == 0) offsets[b] = o;
+  if (tid == 0) {
+    const uint64_t bn = b0 + kPackBlocks;
+    s_start = o;
+    s_end = bn < nb ? blen_prefix[bn] + s_toff[bn / kScanTile == t ? 0 : 1] : (uint32_t)meta[kTotalBits];
+  }
+  __syncthreads();
+#endif
   const uint32_t w0 = s_start >> 5, nwords = ((s_end + 31) >> 5) - w0;
   for (uint32_t i = tid; i < nwords; i += 256) lw[i] = 0;
   uint32_t e[8], nbits = 0;
