@@ -386,6 +386,9 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, 
     cur ^= 1;
     __syncthreads();
   }
+  // the rest needs one thread per symbol: the other 12 waves end here (a finished
+  // wave no longer counts at the workgroup barriers below)
+  if (!sym_thread) return;
   if (n == 0) {
     if (tid == 0) s_bad = (uint32_t)-MH_ERR_EMPTY;
   } else if (n == 1) {  // single symbol -> 1-bit code "0" (HuffmanEncoder.cpp:118-121)
