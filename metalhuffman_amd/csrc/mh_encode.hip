@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/metalhuffman.h"
@@ -36,14 +37,31 @@ constexpr uint32_t kResultBytes = 512;  // mh_encode_frame_device: header, byte 
 constexpr uint32_t kHistParts = MH_HIST_PARTS;  // partial histograms the split workgroups add into
 constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
+constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is published (fused path)
+constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
+#ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
+#define MH_FUSED_MAX_TILES 512
+#endif
 
+#ifndef MH_CODE_STAMPS  // diagnostic builds only: s_memrealtime phase stamps of enc_code_kernel
+#define MH_CODE_STAMPS 0
+#endif
+#if MH_CODE_STAMPS
+constexpr uint32_t kCodeStampWgs = 1024;
+__device__ unsigned long long g_code_stamps[kCodeStampWgs * 8];
+#define MH_CODE_STAMP(wg, k) \
+  if (threadIdx.x == 0 && (wg) < kCodeStampWgs) g_code_stamps[(wg) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define MH_CODE_STAMP(wg, k)
+#endif
 struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint8_t *sym;       // nb * 64 block symbols
   uint32_t *blen;     // nb per-block bit lengths
   uint32_t *tsum;     // ceil(nb / kScanTile) tile sums (then tile offsets)
   uint64_t *hist;     // kHistParts x 256 partial counts
   uint32_t *table;    // 256 x (code_lj16 << 16 | len)
-  uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits]]
+  uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits], [kFlag]]
+  uint16_t *tile_hist;  // fused path: ceil(nb / kCodeTile) x 256 symbol counts
 };
 
 constexpr uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -62,7 +80,9 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
-  o += align256((kTotalBits + 1) * 8);
+  o += align256((kFlag + 1) * 8);
+  if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
+  o += align256((nb + kCodeTile - 1) / kCodeTile * 256 * 2);
   return o;
 }
 
@@ -88,10 +108,20 @@ constexpr uint32_t kSplitBatch = MH_SPLIT_BATCH;
 #define MH_TREE_STAMPS 0
 #endif
 
+// Tiled mode (tile_hist != null, the fused path): workgroup t owns the kCodeTile
+// blocks of tile t (kCodeTile / 32 consecutive groups, loaded at once), stores the
+// tile's symbol counts in tile_hist[t] and re-arms the code kernel's table flag.
+constexpr uint32_t kTileGroups = kCodeTile / 32;
+static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgroup's batch covers a code tile");
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
                                                         uint32_t vec, uint8_t *sym, uint8_t *block_init,
-                                                        uint64_t *hist) {
+                                                        uint64_t *hist, uint16_t *tile_hist, uint64_t *meta) {
+  const bool tiled = tile_hist != nullptr;
+  if (tiled && blockIdx.x == 0 && threadIdx.x == 0) meta[kFlag] = 0;  // the code kernel runs after this one
+#if MH_CODE_STAMPS
+  if (threadIdx.x == 0) atomicMin(&g_code_stamps[1000 * 8 + 0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
   __shared__ uint32_t h[256 * kHistCopies];
   for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
   __syncthreads();
@@ -137,19 +167,30 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
   // flight would leave the frame's read latency-bound
   const uint64_t ngroups = (nb + 31) / 32;
-  for (uint64_t g0 = blockIdx.x; g0 < ngroups; g0 += (uint64_t)kSplitBatch * gridDim.x) {
+  // grid-stride over groups, or (tiled) one batch of consecutive groups
+  const uint64_t ustep = tiled ? 1u : gridDim.x;
+  const uint64_t gfirst = tiled ? (uint64_t)blockIdx.x * kTileGroups : blockIdx.x;
+  const uint64_t gstride = tiled ? ngroups : (uint64_t)kSplitBatch * gridDim.x;
+  for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
+    const uint32_t nu = tiled ? kTileGroups : kSplitBatch;
     uint64_t q[kSplitBatch];
 #pragma unroll
-    for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = load_row(g0 + (uint64_t)u * gridDim.x);
+    for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = u < nu ? load_row(g0 + u * ustep) : 0ull;
 #pragma unroll
     for (uint32_t u = 0; u < kSplitBatch; ++u) {
-      const uint64_t g = g0 + (uint64_t)u * gridDim.x;
-      if (g < ngroups) process(g, q[u]);
+      const uint64_t g = g0 + u * ustep;
+      if (u < nu && g < ngroups) process(g, q[u]);
     }
   }
   __syncthreads();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
+  if (tiled) tile_hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
+#if MH_CODE_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&g_code_stamps[1000 * 8 + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
   // kHistParts partial histograms (workgroups round-robin over them, as over the
   // XCDs): one address per bin would serialise every workgroup's atomic on it
   if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
@@ -209,9 +250,11 @@ __device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
 // (mh_code_lengths' errors, the caller's capacity).
 constexpr uint32_t kTreeThreads = 1024;  // 4 per symbol in the ranking; 256 (one per symbol) elsewhere
 
-__global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, uint8_t *canon_out,
-                                                       uint32_t *table, uint64_t *meta, uint64_t *codes_len_out,
-                                                       uint64_t codes_cap, int32_t *status) {
+// kFused: workgroup 0 of enc_code_kernel -- the table goes out as agent-scope
+// (write-through) stores and meta[kFlag] publishes it to the packing workgroups.
+template <bool kFused>
+__device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta,
+                                          uint64_t *codes_len_out, uint64_t codes_cap, int32_t *status) {
   constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
 #if MH_TREE_STAMPS  // phase timestamps (s_memtime) into meta[2..] for scripts/enc_profile.py
 #define MH_TREE_STAMP(k) \
@@ -440,7 +483,11 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, 
     for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
     e = ((((s_first[L] + rank) << (16 - L)) & 0xFFFFu) << 16) | L;
   }
-  if (sym_thread) table[tid] = e;
+  if constexpr (kFused)
+    __hip_atomic_store(&table[tid], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    table[tid] = e;
+  uint32_t published = 0;
   if (tid == 0) {
     const uint64_t total = s_total;
     const uint64_t len = (total + 7) / 8 + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
@@ -452,8 +499,26 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, 
     meta[kTotalBits] = total;
     if (codes_len_out) *codes_len_out = bad ? 0 : len;
     if (status) *status = bad ? -(int32_t)bad : MH_OK;
+    published = bad ? 2u : 1u;
   }
+  if constexpr (kFused) {
+    // every table store acknowledged (agent scope: past this XCD's L2), then the flag
+    MH_CODE_STAMP(0, 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    MH_CODE_STAMP(0, 2)
+    if (tid == 0)
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), published, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  (void)published;
   MH_TREE_STAMP(8);
+}
+
+__global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, uint8_t *canon_out,
+                                                       uint32_t *table, uint64_t *meta, uint64_t *codes_len_out,
+                                                       uint64_t codes_cap, int32_t *status) {
+  tree_body<false>(hist, canon_out, table, meta, codes_len_out, codes_cap, status);
 }
 
 // Block offsets, one kernel: each workgroup zeroes its share of the code words the
@@ -660,9 +725,245 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
   }
 }
 
+// ---- the fused path: enc_split_kernel (tiled) + enc_code_kernel --------------------
+// One launch replaces tree + scan + pack. Workgroup 0 builds the code table
+// (tree_body<true>) and publishes it through meta[kFlag]; workgroup t + 1 packs tile t
+// (kCodeTile blocks, eight lanes per block, eight symbols each). While the tree is
+// built, a packing workgroup loads its symbols and sums the per-tile histograms of
+// the tiles before it (tile_hist, from the split), so once the table is out its bit
+// offset is a 256-term dot product -- count x code length -- with no exchange between
+// packing workgroups: each waits only for workgroup 0, which is dispatched first, so
+// the launch cannot deadlock however few workgroups are resident. A tile's first code
+// word shares bits with the previous tile's last block (every block has >= 64 bits,
+// a word holds 32): the workgroup computes those bits itself from that block's
+// symbols and writes the word whole; a tile leaves its own partial last word to the
+// next tile (the last tile writes it and the zero pad). Every code word is written
+// exactly once, so the buffer needs no clearing.
+constexpr uint32_t kCodeThreads = 1024;
+#ifndef MH_CODE_MIN_WAVES  // waves per SIMD the register budget must admit (A/B)
+#define MH_CODE_MIN_WAVES 8
+#endif
+constexpr uint32_t kCodeWaves = kCodeThreads / 64;
+constexpr uint32_t kCodeWords = kCodeTile * 64 * 16 / 32 + 2;  // a tile's code words, <= 16-bit codes
+constexpr uint64_t kSpinTicks = 10000000;                       // 100 ms of s_memrealtime (100 MHz)
+static_assert(kCodeThreads == 8 * kCodeTile, "eight lanes per block");
+
+// Inclusive prefix sum over the wave by DPP (row_shr 1/2/4/8 inside each row of 16
+// lanes, then row_bcast 15 / 31 carry the row totals up): no LDS round trip.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// OR the L (1..64) right-aligned bits of v, MSB-first, into the big-endian LDS words
+// lw at bit pos: at most three words, each of which a neighbouring lane may share.
+__device__ __forceinline__ void or_bits(uint32_t *lw, uint32_t pos, uint64_t v, uint32_t L) {
+  const uint64_t a = v << (64u - L);  // left-aligned
+  const uint32_t s = pos & 31u, w = pos >> 5;
+  atomicOr(&lw[w], bswap32((uint32_t)(a >> (32u + s))));
+  if (s + L > 32u) atomicOr(&lw[w + 1], bswap32((uint32_t)(a >> s)));
+  if (s + L > 64u) atomicOr(&lw[w + 2], bswap32((uint32_t)(a << (32u - s))));
+}
+
+__device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const uint16_t *tile_hist,
+                                          const uint32_t *table, uint64_t *meta, uint64_t nb, uint32_t ntiles,
+                                          uint32_t *offsets, uint32_t *words, int32_t *status) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t lw[kCodeWords];
+  __shared__ uint32_t s_cnt[kCodeWaves][256];  // symbol counts of the tiles before this one, per wave
+  __shared__ uint32_t s_dot[4], s_scan[kCodeWaves];
+  __shared__ uint32_t s_flag;
+  const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
+  MH_CODE_STAMP(t + 1, 0)
+  const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
+  const bool on = b < nb;
+  // this lane's 8 symbols and (lanes 0-7, t > 0) the previous block's: in flight
+  // while workgroup 0 builds the tree
+  const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
+  const uint64_t qp = (t > 0 && tid < 8) ? reinterpret_cast<const uint64_t *>(sym + (b0 - 1) * 64)[tid] : 0ull;
+  {
+    // counts of every symbol over tiles [0, t): 16-byte quad q (bins 8q..8q+7) of every
+    // 32nd tile, eight loads in flight per lane (a late tile sums ~400 rows);
+    // lanes l and l + 32 hold the same bins, the 16 waves' partials meet in LDS
+    const uint32_t q4 = tid & 31u, j = tid >> 5;
+#ifdef MH_DIAG_CODE_NOHIST  // timing diagnostics only (wrong output)
+    const uint32_t tlim = 0;
+#else
+    const uint32_t tlim = t;
+#endif
+    const uint4 *th = reinterpret_cast<const uint4 *>(tile_hist);
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t u0 = j; u0 < tlim; u0 += 32u * 8u) {
+      uint4 v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t u = u0 + 32u * k;
+        v[k] = u < tlim ? th[(uint64_t)u * 32 + q4] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          acc[2 * m] += w[m] & 0xFFFFu;
+          acc[2 * m + 1] += w[m] >> 16;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      acc[m] += __shfl_xor(acc[m], 32);
+      if (lane < 32) s_cnt[wave][8 * q4 + m] = acc[m];
+    }
+  }
+  if (tid == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t f;
+    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
+        f = 3u;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_flag = f;
+  }
+  MH_CODE_STAMP(t + 1, 1)
+  __syncthreads();
+  const uint32_t f = s_flag;
+  if (f != 1u) {  // rejected frame (status set by the tree): write nothing
+    if (f == 3u && tid == 0 && status)
+      __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  MH_CODE_STAMP(t + 1, 2)
+  // E = first bit of this tile = sum over symbols of (count before the tile) x length
+  if (wave < 4) {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kCodeWaves; ++j) c += s_cnt[j][tid];
+    const uint32_t x = wave_scan_dpp(c * (tab[tid] & 0xFFu));
+    if (lane == 63) s_dot[wave] = x;
+  }
+  // this lane's codes, as two chunks of four (<= 64 bits each)
+  uint64_t ch[2] = {0, 0};
+  uint32_t cl[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t e = tab[(uint32_t)(q >> (8 * j)) & 0xFFu];
+    const uint32_t len = e & 0xFFu;
+    ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
+    cl[j >> 2] += len;
+  }
+  const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
+  // exclusive scan over the 1024 lanes (lane order = block order, eight lanes each)
+  const uint32_t incl = wave_scan_dpp(nbits);
+  if (lane == 63) s_scan[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
+    if (lane < kCodeWaves) s_scan[lane] = v;
+  }
+  __syncthreads();
+  const uint32_t E = s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
+  const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
+  const uint32_t T = s_scan[kCodeWaves - 1];
+  MH_CODE_STAMP(t + 1, 4)
+  if (on && part == 0) offsets[b] = E + pre;
+  const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
+  const uint32_t nwords = ((end + 31u) >> 5) - w0;
+  for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
+  // the previous block's last r bits, the head of this tile's first word (lanes 0-7)
+  uint32_t head = 0;
+  if (r && wave == 0) {
+    uint32_t lenp = 0;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
+      const uint32_t len = e & 0xFFu;
+      // the lane's codes MSB-first; keep the last 64 bits (r <= 31 of them are used)
+      acc = (acc << len) | ((e >> 16) >> (16 - len));
+      lenp += len;
+    }
+    if (lane >= 8) lenp = 0;
+    // bits of lanes after this one (in block order) = suffix sum over lanes 0-7
+    const uint32_t incp = wave_scan_dpp(lenp);
+    const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
+    // the word's first r bits are the block's last r bits; this lane's code bits end
+    // `after` bits before the block's end, so its last bit is word bit 32 - r + after
+    // (bits that would land before the word fall off the top)
+    if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
+    for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
+  }
+  __syncthreads();
+  if (on) {
+    or_bits(lw, r + pre, ch[0], cl[0]);
+    or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
+  }
+  if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
+  __syncthreads();
+  MH_CODE_STAMP(t + 1, 5)
+  // a partial last word belongs to the next tile (it adds its own first bits); the
+  // last tile writes it, then the zero pad up to the byte count rounded to words
+  const bool last = t + 1 == ntiles;
+  const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
+  for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
+  if (last) {
+    const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
+    for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
+  }
+#if MH_CODE_STAMPS
+  if (tid == 0 && t + 1 < kCodeStampWgs)
+    g_code_stamps[(t + 1) * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
+                                     (unsigned long long)__smid();
+  MH_CODE_STAMP(t + 1, 6)
+  __builtin_amdgcn_s_waitcnt(0);
+  MH_CODE_STAMP(t + 1, 3)
+#endif
+}
+
+__global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kernel(uint64_t *hist, uint8_t *canon_out, uint32_t *table,
+                                                                uint64_t *meta, uint64_t *codes_len_out,
+                                                                uint64_t codes_cap, int32_t *status,
+                                                                const uint8_t *sym, const uint16_t *tile_hist,
+                                                                uint64_t nb, uint32_t ntiles, uint32_t *offsets,
+                                                                uint32_t *words) {
+  static_assert(kTreeThreads == kCodeThreads, "workgroup 0 runs the tree");
+#ifdef MH_DIAG_CODE_NOPACK  // timing diagnostics only (wrong output)
+  if (blockIdx.x != 0) return;
+#endif
+  if (blockIdx.x == 0) {
+    MH_CODE_STAMP(0, 0)
+    tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status);
+    MH_CODE_STAMP(0, 3)
+    return;
+  }
+  pack_tile(blockIdx.x - 1, sym, tile_hist, table, meta, nb, ntiles, offsets, words, status);
+}
+
 }  // namespace
 
 extern "C" {
+
+// MH_ENCODE_KERNELS=4 selects the four-kernel path (split, tree, scan, pack) for
+// every frame size (A/B and tests); frames of more than MH_FUSED_MAX_TILES tiles
+// always take it (a packing workgroup sums the histograms of every tile before it).
+static bool four_kernel_path() {
+  static const bool four = [] {
+    const char *v = std::getenv("MH_ENCODE_KERNELS");
+    return v && std::strcmp(v, "4") == 0;
+  }();
+  return four;
+}
 
 // mh_encode_frame_device_async's workspace; mh_encode_frame_device needs kResultBytes
 // more (see mh_encode_workspace_bytes in the header: it reports the larger figure).
@@ -670,6 +971,20 @@ static size_t async_workspace_bytes(uint32_t width, uint32_t height) {
   const uint64_t nb = (uint64_t)((width + 7) / 8) * ((height + 7) / 8);
   return (size_t)carve(nullptr, nb, nullptr);
 }
+
+#if MH_CODE_STAMPS
+int mh_diag_code_stamps_reset(void) {
+  static unsigned long long z[kCodeStampWgs * 8];
+  for (auto &v : z) v = 0;
+  z[1000 * 8] = ~0ull;  // split start: a minimum
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_code_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+int mh_diag_code_stamps(unsigned long long *host, size_t n) {
+  if (n > kCodeStampWgs * 8) n = kCodeStampWgs * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_code_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+#endif
 
 size_t mh_encode_workspace_bytes(uint32_t width, uint32_t height) {
   return async_workspace_bytes(width, height) + kResultBytes;
@@ -699,9 +1014,19 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
     return MH_ERR_HIP;
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  if (ncode <= MH_FUSED_MAX_TILES && !four_kernel_path()) {
+    // two launches: the tiled split, then tree + offsets + packing in one kernel
+    hipLaunchKernelGGL(enc_split_kernel, dim3((uint32_t)ncode), dim3(256), 0, s, d_gray, width, height, bw, nb,
+                       flags, vec, w.sym, d_block_init, w.hist, w.tile_hist, w.meta);
+    hipLaunchKernelGGL(enc_code_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist,
+                       d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, w.sym, w.tile_hist, nb,
+                       (uint32_t)ncode, d_block_offsets, reinterpret_cast<uint32_t *>(d_codes));
+    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
+  }
   const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, MH_SPLIT_WGS);
   hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
-                     w.sym, d_block_init, w.hist);
+                     w.sym, d_block_init, w.hist, nullptr, w.meta);
   hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
                      d_codes_len, codes_cap, d_status);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,

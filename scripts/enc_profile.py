@@ -24,6 +24,22 @@ for k in range(reps):
 torch.cuda.synchronize()
 print(f"async encode {1e6 * (time.perf_counter() - t0) / reps:.1f} us/frame")
 
+# the same encodes enqueued behind bench.py's launch gate before the clock starts:
+# device time per frame without the host's enqueue cost (Python + 4 launches)
+from bench import GATE  # noqa: E402
+if GATE.ok():
+    for rep in range(2):
+        torch.cuda.synchronize()
+        GATE.arm(torch.cuda.current_stream().cuda_stream)
+        te = time.perf_counter()
+        for k in range(reps):
+            enc.encode_async(imgs[k % 4], codes=codes[k % 4])
+        t0 = time.perf_counter()
+        print(f"host enqueue {1e6 * (t0 - te) / reps:.1f} us/frame")
+        GATE.open()
+        torch.cuda.synchronize()
+        print(f"gated async encode {1e6 * (time.perf_counter() - t0) / reps:.1f} us/frame")
+
 if len(sys.argv) > 2 and sys.argv[2] == "stamps":
     # library built with -DMH_TREE_STAMPS=1: s_memtime at the tree kernel's phase
     # boundaries in meta[2..10] (meta = the last 256 bytes of the async workspace)
