@@ -235,6 +235,14 @@ __device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
   key = take ? p : key;
 }
 
+// ... on 32-bit keys (frames of < 2^22 symbols, see tree_body)
+template <uint32_t D>
+__device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
+  const uint32_t p = xor_partner<D>(lane, key);
+  const bool take = (p < key) != ((lane & D) != 0u);  // keys are distinct
+  key = take ? p : key;
+}
+
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
 // from the 256 counts. The reference keeps every node in one array sorted by weight,
 // inserts at upper_bound (a new node goes after all nodes of equal weight) and merges
@@ -252,10 +260,15 @@ constexpr uint32_t kTreeThreads = 1024;  // 4 per symbol in the ranking; 256 (on
 
 // kFused: workgroup 0 of enc_code_kernel -- the table goes out as agent-scope
 // (write-through) stores and meta[kFlag] publishes it to the packing workgroups.
+// nsym: the frame's symbol count (64 per block). Below 2^22 - 1 every weight --
+// root included -- fits 22 bits, and the ranking and merge keys fit 32 bits.
 template <bool kFused>
 __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta,
-                                          uint64_t *codes_len_out, uint64_t codes_cap, int32_t *status) {
+                                          uint64_t *codes_len_out, uint64_t codes_cap, int32_t *status,
+                                          uint64_t nsym) {
   constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
+  constexpr uint32_t kW32End = (1u << 22) - 1u;  // 32-bit merge keys: an empty slot's weight
+  const bool k32 = nsym < (uint64_t)kW32End;
 #if MH_TREE_STAMPS  // phase timestamps (s_memtime) into meta[2..] for scripts/enc_profile.py
 #define MH_TREE_STAMP(k) \
   if (tid == 0) meta[2 + (k)] = __builtin_amdgcn_s_memtime();
@@ -268,6 +281,7 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   __shared__ uint32_t s_qv[64], s_qid[64];
 #endif
   __shared__ __attribute__((aligned(16))) uint64_t s_key[256];
+  __shared__ __attribute__((aligned(16))) uint32_t s_key32[256];
   __shared__ uint32_t s_leaf_sym[256], s_len[256], s_par[2][512], s_dep[2][512];
   __shared__ uint32_t s_wcnt[4][17], s_first[17], s_n, s_bad;
   __shared__ uint32_t s_below[4][256];
@@ -299,17 +313,29 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     // have key 0, below every present one: subtract their count afterwards.
     // Four threads per symbol, a quarter of the keys each (the compares are VALU
     // issue-bound: one wave per SIMD took 6 K clocks for all 256).
-    if (sym_thread) s_key[tid] = f ? (f << 8) | tid : 0;
-    const uint32_t present = (uint32_t)__syncthreads_count(f != 0);
     const uint32_t ks = tid & 255u, part = tid >> 8;
-    const uint64_t key = s_key[ks];
-    uint32_t below = 0;
-    const ulonglong2 *kv = reinterpret_cast<const ulonglong2 *>(s_key) + part * 32u;
+    uint32_t below = 0, present;
+    if (k32) {  // counts < 2^22: (count << 8 | symbol) fits 32 bits
+      if (sym_thread) s_key32[tid] = f ? (uint32_t)(f << 8) | tid : 0u;
+      present = (uint32_t)__syncthreads_count(f != 0);
+      const uint32_t key = s_key32[ks];
+      const uint4 *kv = reinterpret_cast<const uint4 *>(s_key32) + part * 16u;
+#pragma unroll
+      for (uint32_t t = 0; t < 16; ++t) {  // same address across the wave: broadcast reads
+        const uint4 v = kv[t];
+        below += (v.x < key ? 1u : 0u) + (v.y < key ? 1u : 0u) + (v.z < key ? 1u : 0u) + (v.w < key ? 1u : 0u);
+      }
+    } else {
+      if (sym_thread) s_key[tid] = f ? (f << 8) | tid : 0;
+      present = (uint32_t)__syncthreads_count(f != 0);
+      const uint64_t key = s_key[ks];
+      const ulonglong2 *kv = reinterpret_cast<const ulonglong2 *>(s_key) + part * 32u;
 #pragma unroll 16
-    for (uint32_t t = 0; t < 32; ++t) {  // same address across the wave: broadcast reads
-      const ulonglong2 v = kv[t];
-      below += v.x < key ? 1u : 0u;
-      below += v.y < key ? 1u : 0u;
+      for (uint32_t t = 0; t < 32; ++t) {  // same address across the wave: broadcast reads
+        const ulonglong2 v = kv[t];
+        below += v.x < key ? 1u : 0u;
+        below += v.y < key ? 1u : 0u;
+      }
     }
     s_below[part][ks] = below;
     __syncthreads();
@@ -346,20 +372,32 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
       // keeps its order). min(A[i], B[63 - i]) holds the 64 smallest of both heads as
       // a bitonic sequence; six half-cleaner stages (partners from permlane32_swap,
       // ds_swizzle and DPP -- no LDS round trip) sort it.
-      uint64_t key;
-      {
-        const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + 63u - lane];
-        const bool a = lv <= iv;  // equal weight: the leaf (type 0) first
-        key = ((uint64_t)(a ? lv : iv) << 32) | (a ? li + lane : (0x10000u | (ii + 63u - lane)));
+      uint32_t q, qid;
+      const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + 63u - lane];
+      const bool a = lv <= iv;  // equal weight: the leaf (type 0) first
+      if (k32) {
+        // weight (22 bits; an empty slot saturates above every real weight) : type : position (9 bits)
+        uint32_t key = (min(a ? lv : iv, kW32End) << 10) | (a ? li + lane : (0x200u | (ii + 63u - lane)));
+        bitonic_stage32<32>(lane, key);
+        bitonic_stage32<16>(lane, key);
+        bitonic_stage32<8>(lane, key);
+        bitonic_stage32<4>(lane, key);
+        bitonic_stage32<2>(lane, key);
+        bitonic_stage32<1>(lane, key);
+        q = key >> 10;
+        qid = (key & 0x200u) ? n + (key & 0x1FFu) : (key & 0x1FFu);
+      } else {
+        uint64_t key = ((uint64_t)(a ? lv : iv) << 32) | (a ? li + lane : (0x10000u | (ii + 63u - lane)));
+        bitonic_stage<32>(lane, key);
+        bitonic_stage<16>(lane, key);
+        bitonic_stage<8>(lane, key);
+        bitonic_stage<4>(lane, key);
+        bitonic_stage<2>(lane, key);
+        bitonic_stage<1>(lane, key);
+        q = (uint32_t)(key >> 32);
+        const uint32_t kl = (uint32_t)key;
+        qid = (kl & 0x10000u) ? n + (kl & 0xFFFFu) : kl;
       }
-      bitonic_stage<32>(lane, key);
-      bitonic_stage<16>(lane, key);
-      bitonic_stage<8>(lane, key);
-      bitonic_stage<4>(lane, key);
-      bitonic_stage<2>(lane, key);
-      bitonic_stage<1>(lane, key);
-      const uint32_t q = (uint32_t)(key >> 32), kl = (uint32_t)key;
-      const uint32_t qid = (kl & 0x10000u) ? n + (kl & 0xFFFFu) : kl;
 #else
       const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + lane];
       uint32_t rl = 0, ri = 0;  // internal candidates < lv; leaf candidates <= iv
@@ -417,10 +455,10 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   }
   __syncthreads();
   MH_TREE_STAMP(4);
-  // 5 rounds: a node within 31 hops of the root gets its exact depth; any other is
-  // at least 32 deep, above the 16-bit limit either way (MH_ERR_CODE_TOO_LONG)
+  // 4 rounds: a node within 16 hops of the root gets its exact depth and the root as
+  // its ancestor; any other is deeper than 16 (MH_ERR_CODE_TOO_LONG)
   uint32_t cur = 0;
-  for (uint32_t step = 0; step < 5; ++step) {
+  for (uint32_t step = 0; step < 4; ++step) {
     for (uint32_t i = tid; i < nodes; i += kTreeThreads) {
       const uint32_t p = s_par[cur][i];
       s_dep[cur ^ 1][i] = s_dep[cur][i] + s_dep[cur][p];
@@ -437,9 +475,9 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   } else if (n == 1) {  // single symbol -> 1-bit code "0" (HuffmanEncoder.cpp:118-121)
     if (tid == 0) s_len[s_leaf_sym[0]] = 1;
   } else if (tid < n) {
-    const uint32_t d = s_dep[cur][tid];
+    const uint32_t d = s_par[cur][tid] == root ? s_dep[cur][tid] : 17u;
     if (d > 16) s_bad = (uint32_t)-MH_ERR_CODE_TOO_LONG;
-    s_len[s_leaf_sym[tid]] = min(d, 255u);
+    s_len[s_leaf_sym[tid]] = d;
   }
   __syncthreads();
   MH_TREE_STAMP(5);
@@ -517,8 +555,8 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
 
 __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, uint8_t *canon_out,
                                                        uint32_t *table, uint64_t *meta, uint64_t *codes_len_out,
-                                                       uint64_t codes_cap, int32_t *status) {
-  tree_body<false>(hist, canon_out, table, meta, codes_len_out, codes_cap, status);
+                                                       uint64_t codes_cap, int32_t *status, uint64_t nsym) {
+  tree_body<false>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nsym);
 }
 
 // Block offsets, one kernel: each workgroup zeroes its share of the code words the
@@ -943,7 +981,7 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kern
 #endif
   if (blockIdx.x == 0) {
     MH_CODE_STAMP(0, 0)
-    tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status);
+    tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
     MH_CODE_STAMP(0, 3)
     return;
   }
@@ -1028,7 +1066,7 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
                      w.sym, d_block_init, w.hist, nullptr, w.meta);
   hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
-                     d_codes_len, codes_cap, d_status);
+                     d_codes_len, codes_cap, d_status, nb * 64);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
                      w.tsum, w.meta, reinterpret_cast<uint32_t *>(d_codes));
   hipLaunchKernelGGL(enc_pack_kernel, dim3((uint32_t)((nb + kPackBlocks - 1) / kPackBlocks)), dim3(256), 0, s, w.sym, w.table, w.blen, w.tsum, nb,

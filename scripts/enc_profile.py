@@ -42,11 +42,14 @@ if GATE.ok():
 
 if len(sys.argv) > 2 and sys.argv[2] == "stamps":
     # library built with -DMH_TREE_STAMPS=1: s_memtime at the tree kernel's phase
-    # boundaries in meta[2..10] (meta = the last 256 bytes of the async workspace)
+    # boundaries in meta[2..10] (either path: the tree runs in enc_tree_kernel or workgroup 0)
     from metalhuffman_amd import _native as N
-    ws = int(N.lib().mh_encode_workspace_bytes(bb.shape[1], bb.shape[0]))
+    # meta's offset in the workspace: mh_encode.hip carve() (sym, blen, tsum, hist, table, meta)
+    a256 = lambda x: (x + 255) // 256 * 256
+    nb = ((bb.shape[1] + 7) // 8) * ((bb.shape[0] + 7) // 8)
+    moff = a256(nb * 64) + a256(nb * 4) + a256((nb + 255) // 256 * 4) + a256(8 * 256 * 8) + a256(256 * 4)
     base = enc.workspace.data_ptr()
-    off = (base + 255) // 256 * 256 - base + (ws - 512) - 256
+    off = (base + 255) // 256 * 256 - base + moff
     for k in range(3):
         enc.encode_async(imgs[k], codes=codes[k])
         torch.cuda.synchronize()

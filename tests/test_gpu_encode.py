@@ -55,6 +55,20 @@ def test_encode_8192_tile(mh, device, bigbridge):
     _check(mh, device, F.mirror_tile(bigbridge, 8192, 8192))
 
 
+@pytest.mark.parametrize("hw", [(2048, 2048), (2056, 2048), (8, 65528), (2048, 1536)])
+def test_async_encode_fused_path_boundary(mh, device, bigbridge, hw):
+    """Frames of up to 512 tiles of 128 blocks take the two-launch path (tiled split +
+    code kernel), larger ones the four-kernel path. (h, w) = (2048, 2048) is exactly
+    512 tiles, (2056, 2048) 514, (8, 65528) one block row of 8191 blocks (64 tiles,
+    the last partial), (2048, 1536) BigBridge's shape transposed. Both sides
+    byte-identical to the host codec."""
+    from metalhuffman_amd import frames as F
+    h, w = hw
+    img = np.ascontiguousarray(F.mirror_tile(bigbridge, h, w)) if h > 8 else \
+        np.ascontiguousarray(np.tile(bigbridge[:8], (1, w // bigbridge.shape[1] + 1))[:, :w])
+    _check_async(mh, device, img)
+
+
 def test_encode_too_long_code_is_rejected(mh, device):
     import torch
     from metalhuffman_amd.encoder import encode_frame_device
