@@ -1177,7 +1177,11 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
   if (nw < 1) nw = 1;
   if (nw > (uint32_t)kMaxWavesPerWG) nw = kMaxWavesPerWG;
   a.n_groups = (a.total_tiles + nw - 1) / nw;
+#ifdef MH_GRID_WGS_PER_CU  // A/B: cap the persistent grid below the occupancy limit
+  const uint32_t resident = (uint32_t)(cus * min(di->occ[kDelta ? 1 : 0][nw], MH_GRID_WGS_PER_CU));
+#else
   const uint32_t resident = (uint32_t)(cus * di->occ[kDelta ? 1 : 0][nw]);
+#endif
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
   hipLaunchKernelGGL(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), 0, s, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
