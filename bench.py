@@ -182,6 +182,9 @@ class Workload:
             wb.record()
             torch.cuda.synchronize(dev)
             print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
+        # eager behind the gate only while the K packets surely fit the HW queue
+        # (a full queue would block the enqueue until the gate expires)
+        eager_gated = GATED_EAGER and steps <= 256
         def timed(gated):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
@@ -195,7 +198,7 @@ class Workload:
                 GATE.arm(torch.cuda.current_stream(dev).cuda_stream)
             if gated or graph is not None:
                 r0.record()
-                if graph is not None:
+                if graph is not None and not (gated and eager_gated):
                     graph.replay()
                 else:
                     for i in range(steps):
@@ -228,9 +231,11 @@ class Workload:
             timed(True)  # the gate's own first launch off the clock
             wall, region_ms = timed(True)
             self.ungated_wall, _ = timed(False)
+            self.timed_launch = "eager behind the launch gate" if eager_gated else "hipGraph behind the launch gate"
         else:
             wall, region_ms = timed(False)
             self.ungated_wall = None
+            self.timed_launch = "hipGraph" if graph is not None else "eager"
         # Per-launch kernel duration: the same K-launch graph replayed back to back
         # (>= 200 launches) between one event pair on the launch stream, so the fixed
         # cost of opening a region (gate release, first dispatch: ~13 us measured)
@@ -319,6 +324,13 @@ class _Gate:
 
 
 GATE = _Gate()
+# Gated regions enqueue the K launches one by one (eager) rather than as one graph
+# replay: both are queued before the clock starts, but a replayed graph's first
+# kernel started ~6 us after the gate (rocprofv3 trace; a cross-queue wait), so at
+# the driver's 20 steps eager measured 477-483 vs 470-474 x10^3 MB/s interleaved on
+# one box (profiles/r02_v10_gated_eager_vs_graph_ab.txt). MH_BENCH_GATED_LAUNCH=graph
+# restores the replay.
+GATED_EAGER = os.environ.get("MH_BENCH_GATED_LAUNCH", "eager") == "eager"
 
 
 def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None, read_bytes=None,
@@ -759,7 +771,7 @@ def main(argv=None) -> int:
                 f"{args.frames} distinct frames resident per GPU, shared canonical table",
         "config": {"workload": wdesc, "width": int(ref_shape[1]), "height": int(ref_shape[0]),
                    "frames_per_step_per_gpu": int(wl.launches[0].n_frames),
-                   "parallelism": f"frame-sharded x{world}", "launch": "hipGraph" if not args.no_graph else "eager"},
+                   "parallelism": f"frame-sharded x{world}", "launch": wl.timed_launch},
         "mpixels_per_s": round(value, 1),
         "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload, wl.read_bytes,
                              wl.kernel_ms),

@@ -49,9 +49,13 @@ constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (sp
 #if MH_CODE_STAMPS
 constexpr uint32_t kCodeStampWgs = 1024;
 __device__ unsigned long long g_code_stamps[kCodeStampWgs * 8];
+__device__ unsigned long long g_split_stamps[kCodeStampWgs * 8];
+#define MH_SPLIT_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < kCodeStampWgs) g_split_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #define MH_CODE_STAMP(wg, k) \
   if (threadIdx.x == 0 && (wg) < kCodeStampWgs) g_code_stamps[(wg) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
+#define MH_SPLIT_STAMP(k)
 #define MH_CODE_STAMP(wg, k)
 #endif
 struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
@@ -119,9 +123,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
                                                         uint64_t *hist, uint16_t *tile_hist, uint64_t *meta) {
   const bool tiled = tile_hist != nullptr;
   if (tiled && blockIdx.x == 0 && threadIdx.x == 0) meta[kFlag] = 0;  // the code kernel runs after this one
-#if MH_CODE_STAMPS
-  if (threadIdx.x == 0) atomicMin(&g_code_stamps[1000 * 8 + 0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+  MH_SPLIT_STAMP(0)
   __shared__ uint32_t h[256 * kHistCopies];
   for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
   __syncthreads();
@@ -176,24 +178,29 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     uint64_t q[kSplitBatch];
 #pragma unroll
     for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = u < nu ? load_row(g0 + u * ustep) : 0ull;
+#if MH_CODE_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    MH_SPLIT_STAMP(1)
+#endif
 #pragma unroll
     for (uint32_t u = 0; u < kSplitBatch; ++u) {
       const uint64_t g = g0 + u * ustep;
       if (u < nu && g < ngroups) process(g, q[u]);
     }
   }
+  MH_SPLIT_STAMP(2)
   __syncthreads();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
   if (tiled) tile_hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
-#if MH_CODE_STAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) atomicMax(&g_code_stamps[1000 * 8 + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+  MH_SPLIT_STAMP(3)
   // kHistParts partial histograms (workgroups round-robin over them, as over the
   // XCDs): one address per bin would serialise every workgroup's atomic on it
   if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
+#if MH_CODE_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  MH_SPLIT_STAMP(4)
+#endif
 }
 
 #ifndef MH_SCAN_TICKET   // 1: the scan's last workgroup (completion ticket) scans the tile totals;
@@ -1014,12 +1021,19 @@ static size_t async_workspace_bytes(uint32_t width, uint32_t height) {
 int mh_diag_code_stamps_reset(void) {
   static unsigned long long z[kCodeStampWgs * 8];
   for (auto &v : z) v = 0;
-  z[1000 * 8] = ~0ull;  // split start: a minimum
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_code_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_code_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess &&
+                 hipMemcpyToSymbol(HIP_SYMBOL(g_split_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess
+             ? 0
+             : -1;
 }
 int mh_diag_code_stamps(unsigned long long *host, size_t n) {
   if (n > kCodeStampWgs * 8) n = kCodeStampWgs * 8;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_code_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+int mh_diag_split_stamps(unsigned long long *host, size_t n) {
+  if (n > kCodeStampWgs * 8) n = kCodeStampWgs * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_split_stamps), n * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif

@@ -18,6 +18,7 @@ img = torch.from_numpy(F.block_shuffle(bb, 901)).to(dev)
 enc = Encoder(bb.shape[1], bb.shape[0], dev)
 lib = N.lib()
 lib.mh_diag_code_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+lib.mh_diag_split_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 nwg = 1 + (enc.nb + 127) // 128
 imgs = [torch.from_numpy(F.block_shuffle(bb, 900 + k)).to(dev) for k in range(4)]
 codes = [torch.empty(enc.cap, dtype=torch.uint8, device=dev) for _ in range(4)]
@@ -32,7 +33,9 @@ for rep in range(6):
     torch.cuda.synchronize()
     st = np.zeros(1024 * 8, np.uint64)
     lib.mh_diag_code_stamps(st.ctypes.data, st.size)
-    sp = st[1000 * 8: 1000 * 8 + 2].astype(np.int64)
+    ss = np.zeros(1024 * 8, np.uint64)
+    lib.mh_diag_split_stamps(ss.ctypes.data, ss.size)
+    ss = ss.reshape(1024, 8)[: nwg - 1, :5].astype(np.int64)
     st = st.reshape(1024, 8)[:nwg].astype(np.int64)
     ids = st[1:, 7].copy()
     st[:, 7] = 0
@@ -40,7 +43,11 @@ for rep in range(6):
     us = (st - t0) / 100.0
     p = us[1:]
     q = lambda a: f"{np.min(a):6.2f} {np.median(a):6.2f} {np.max(a):6.2f}"
-    print(f"rep {rep}: split first start {(sp[0] - t0) / 100:.2f} last end {(sp[1] - t0) / 100:.2f} us")
+    s0 = ss[:, 0].min()
+    sq = lambda a: f"{np.min(a):6.2f} {np.median(a):6.2f} {np.max(a):6.2f}"
+    ssu = (ss - s0) / 100.0
+    print(f"rep {rep}: split (us from its first workgroup) start {sq(ssu[:,0])} loaded {sq(ssu[:,1])}"
+          f" counted {sq(ssu[:,2])} reduced {sq(ssu[:,3])} end {sq(ssu[:,4])}; code wg0 start at {(t0 - s0) / 100:.2f}")
     print(f"rep {rep}: wg0 tree done {us[0,1]:.2f} flag-store {us[0,2]:.2f} end {us[0,3]:.2f} us")
     print(f"   pack start  min/med/max {q(p[:,0])}")
     print(f"   flag seen   {q(p[:,1])}")
