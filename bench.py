@@ -182,9 +182,10 @@ class Workload:
             wb.record()
             torch.cuda.synchronize(dev)
             print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
-        # eager behind the gate only while the K packets surely fit the HW queue
-        # (a full queue would block the enqueue until the gate expires)
-        eager_gated = GATED_EAGER and steps <= 256
+        # eager behind the gate for short regions only: there the replayed graph's ~6 us
+        # start costs most; over 256 launches of the 64-frame batch the eager dispatches
+        # ran 68.2 vs 63.6 us each (graph), so long regions keep the replay
+        eager_gated = GATED_EAGER and steps <= 64
         def timed(gated):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
