@@ -4,15 +4,17 @@
 //   split + deltas   Shared/Util.m:233-323, Shared/AAPLRenderer.m:432-515 (eight lanes
 //                    per 8x8 block, zero padding past W/H, optional init byte :449-473)
 //   histogram        HuffmanEncoder.cpp:310-330 (symbol counts; LDS, then global atomics
-//                    into kHistParts partial histograms)            -> enc_split_kernel
+//                    into kHistParts partial histograms, and per-tile counts)
 //   code lengths     HuffmanEncoder.cpp:29-145 -- the reference's sorted node array with
 //                    upper_bound insertion is the two-queue Huffman merge with ties going
 //                    to the leaf queue, run in batched rounds; then canonical codes
-//                    huff_util.hpp:94-193 and the code byte count   -> enc_tree_kernel
+//                    huff_util.hpp:94-193 and the code byte count
 //   block offsets    HuffmanUtil.cpp:1103-1128 -- an exclusive prefix sum of the
-//                    per-block code-length sums                     -> enc_scan_kernel
-//   bit packing      HuffmanEncoder.cpp:211-381 -- MSB-first, eight lanes per block,
-//                    staged per workgroup in LDS                    -> enc_pack_kernel
+//                    per-block code-length sums
+//   bit packing      HuffmanEncoder.cpp:211-381 -- MSB-first, staged per workgroup in LDS
+// Frames of <= MH_FUSED_MAX_TILES tiles: two launches, enc_split_kernel (tiled) and
+// enc_code_kernel (workgroup 0 = tree, the others = offsets + packing of one tile each).
+// Larger frames: enc_split_kernel, enc_tree_kernel, enc_scan_kernel, enc_pack_kernel.
 // mh_encode_frame_device_async never synchronises (header, code bytes and status are
 // written to device memory); mh_encode_frame_device runs it and synchronises once at
 // the end to return the header and the byte count on the host.
