@@ -24,13 +24,17 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--tag", default="")
+ap.add_argument("--tile8192", action="store_true", help="config 3: one 8192x8192 BigBridge mirror tile")
 args = ap.parse_args()
 
 lib = N.lib()
 if not hasattr(lib, "mh_diag_stamps"):
     sys.exit("not a MH_DIAG_STAMPS build (set MH_LIB)")
 bb = F.bigbridge()
-efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.batch)]
+if args.tile8192:
+    efs = [mh.encode_frame(F.mirror_tile(bb, 8192, 8192))]
+else:
+    efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.batch)]
 t1, t2 = efs[0].tables()
 tabs = D.DeviceTables.upload(t1, t2, "cuda")
 fr = D.DeviceFrames.pack(efs, "cuda")
@@ -55,6 +59,8 @@ names = ["entry", "hdr", "lut", "staged", "tile0", "loop", "drain"]
 for i, nm in enumerate(names):
     v = (st[:, i].astype(np.int64) - int(t0)) * 0.01
     print(f"{nm:7s} us  min {v.min():7.2f}  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}  max {v.max():7.2f}")
+loop_end = (st[:, 5].astype(np.int64) - int(t0)) * 0.01
+print("loop end per wave: p10 %.2f p50 %.2f p90 %.2f p99 %.2f max %.2f us" % tuple(np.percentile(loop_end, [10, 50, 90, 99, 100])))
 for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6)]:
     d = (st[:, b].astype(np.int64) - st[:, a].astype(np.int64)) * 0.01
     print(f"{names[a]}->{names[b]:7s} p50 {np.median(d):7.2f}  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f}")
