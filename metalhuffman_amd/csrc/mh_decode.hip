@@ -76,6 +76,9 @@ namespace {
 #ifndef MH_LP_MIN_BITS          // lane-pair variant: blocks shorter than 2x this decode on one lane
 #define MH_LP_MIN_BITS 16
 #endif
+#ifndef MH_LUT_FIRST            // 1: batch kernel issues the table's loads before the first header (A/B)
+#define MH_LUT_FIRST 0
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -619,6 +622,32 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
+#if MH_LUT_FIRST
+  // The table's L2 loads go out before the first header's HBM load, so waiting for
+  // them (vmcnt counts in issue order) does not wait for the header: the table is in
+  // LDS, and the workgroup barrier passed, while the headers are still in flight.
+  constexpr uint32_t kLutChunks = kLutBytes / 16, kLutPer = 4;
+  const bool lut_regs = a.lut && blockDim.x * kLutPer >= kLutChunks;  // >= 5 waves
+  if (lut_regs) {
+    const __amdgpu_buffer_rsrc_t rl = uniform_rsrc(a.lut, (uint32_t)kLutBytes);
+    v4u32 L[kLutPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kLutPer; ++k)
+      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * blockDim.x) * 16u), 0, 0);
+    hdr_issue(a, t0, lane, hc);
+    v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
+#pragma unroll
+    for (uint32_t k = 0; k < kLutPer; ++k)
+      if (threadIdx.x + k * blockDim.x < kLutChunks) dstv[threadIdx.x + k * blockDim.x] = L[k];
+  } else {
+    hdr_issue(a, t0, lane, hc);
+    if (a.lut) {
+      const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
+      v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
+      for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
+    }
+  }
+#else
   hdr_issue(a, t0, lane, hc);
 
   // ---- lookup table into LDS (shared by the workgroup) ----
@@ -627,6 +656,7 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
     for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
   }
+#endif
 
   v4u32 R[kStageChunks];
   Tile cur = hdr_resolve(a, hc, lane);
