@@ -212,7 +212,7 @@ class Workload:
         # start costs most; over 256 launches of the 64-frame batch the eager dispatches
         # ran 68.2 vs 63.6 us each (graph), so long regions keep the replay
         eager_gated = GATED_EAGER and steps <= 64
-        def timed(gated):
+        def timed(gated, events=True):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
             opening synchronize, and the clock starts when the host opens it -- every
@@ -224,13 +224,15 @@ class Workload:
             if gated:
                 GATE.arm(torch.cuda.current_stream(dev).cuda_stream)
             if gated or graph is not None:
-                r0.record()
+                if events:
+                    r0.record()
                 if graph is not None and not (gated and eager_gated):
                     graph.replay()
                 else:
                     for i in range(steps):
                         self.launch(i)
-                r1.record()
+                if events:
+                    r1.record()
             # (no barrier while a gate is armed: an RCCL barrier would queue behind it;
             # each rank times its own region, the max over ranks is taken below)
             t0 = time.perf_counter()
@@ -252,11 +254,19 @@ class Workload:
                 t = torch.tensor([w], dtype=torch.float64, device=on)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 w = float(t.item())
-            return w, r0.elapsed_time(r1)
+            return w, (r0.elapsed_time(r1) if events else None)
 
         if gate and GATE.ok():
             timed(True)  # the gate's own first launch off the clock
-            wall, region_ms = timed(True)
+            # The clocked region holds only the K launches: its two HIP event records
+            # (markers in the queue) cost ~7 us per region at 20 steps (510 vs 482 x10^3
+            # MB/s interleaved, profiles/r02_v13_region_events_ab.txt), so the event-timed
+            # region is a second, identical one. MH_BENCH_REGION_EVENTS=1 keeps them inside.
+            if os.environ.get("MH_BENCH_REGION_EVENTS", "0") == "0":
+                wall, _ = timed(True, events=False)
+                _, region_ms = timed(True)
+            else:
+                wall, region_ms = timed(True)
             self.ungated_wall, _ = timed(False)
             self.timed_launch = "eager behind the launch gate" if eager_gated else "hipGraph behind the launch gate"
         else:
@@ -337,6 +347,16 @@ class _Gate:
         return True
 
     def arm(self, stream: int) -> None:
+        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "busy":  # A/B: CUs kept busy while closed
+            import ctypes
+            if not hasattr(self, "_dflag"):
+                self._dflag = torch.zeros(64, dtype=torch.int32, device="cuda")
+                self.lib.gate_arm_busy.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
+            nwg = int(os.environ.get("MH_BENCH_GATE_WGS", "1024"))
+            if self.lib.gate_arm_busy(self.h, self.d, self._dflag.data_ptr(), stream, 200_000, nwg,
+                                      self._dflag.data_ptr() + 128) != 0:
+                raise RuntimeError("launch gate: busy kernel launch failed")
+            return
         if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "wait":  # A/B: stream wait on the flag
             import ctypes
             self.lib.gate_arm_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]

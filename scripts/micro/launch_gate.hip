@@ -22,9 +22,41 @@ __global__ void __launch_bounds__(64) gate_kernel(const unsigned *flag, unsigned
   }
 }
 
+// Busy variant (A/B): every workgroup keeps its CU issuing ALU work while the gate is
+// closed (so the clocks do not settle down during the host's enqueue); workgroup 0's
+// first lane polls the host flag and raises a device flag the others watch.
+__global__ void __launch_bounds__(64) gate_busy_kernel(const unsigned *flag, unsigned *dflag,
+                                                       unsigned long long max_ticks, float *sink) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  float x = (float)threadIdx.x, y = 1.0001f;
+  for (;;) {
+    unsigned open;
+    if (blockIdx.x == 0) {
+      open = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (open && threadIdx.x == 0) __hip_atomic_store(dflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      open = __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane(open) || __builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x = __builtin_fmaf(x, y, 0.5f);
+  }
+  if (x == 12345.0f) sink[threadIdx.x] = x;  // keeps the ALU loop
+}
+
 }  // namespace
 
 extern "C" {
+
+// Busy gate on `stream`: `nwg` one-wave workgroups; dflag is a device word (cleared here).
+int gate_arm_busy(unsigned *host_ptr, const unsigned *dev_ptr, unsigned *dflag, void *stream, unsigned max_us,
+                  unsigned nwg, float *sink) {
+  __atomic_store_n(host_ptr, 0u, __ATOMIC_SEQ_CST);
+  if (hipMemsetAsync(dflag, 0, 4, (hipStream_t)stream) != hipSuccess) return -1;
+  hipLaunchKernelGGL(gate_busy_kernel, dim3(nwg), dim3(64), 0, (hipStream_t)stream, dev_ptr, dflag,
+                     (unsigned long long)max_us * 100ull, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // A host-mapped, coherent flag word; *host_ptr is written by the host, the kernel
 // polls *dev_ptr.
