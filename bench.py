@@ -279,15 +279,24 @@ class Workload:
         # is amortised as in rocprofv3's per-dispatch durations of the same launches.
         self.region_kernel_ms = region_ms / steps
         if graph is not None:
-            reps = max(1, -(-200 // steps))
+            # one graph of >= 200 launches (a replayed graph's first kernel starts ~6 us
+            # late: 10 replays of a 20-launch graph would add ~0.3 us per launch)
+            kg, nk = graph, steps
+            if steps < 200:
+                nk = 200
+                kg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(kg):
+                    for i in range(nk):
+                        self.launch(i)
+                kg.replay()
             ka, kb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize(dev)
             ka.record()
-            for _ in range(reps):
-                graph.replay()
+            kg.replay()
             kb.record()
             torch.cuda.synchronize(dev)
-            self.kernel_ms = ka.elapsed_time(kb) / (reps * steps)
+            self.kernel_ms = ka.elapsed_time(kb) / nk
+            del kg
         else:
             self.kernel_ms = self.region_kernel_ms
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
