@@ -366,6 +366,12 @@ class _Gate:
                                       self._dflag.data_ptr() + 128) != 0:
                 raise RuntimeError("launch gate: busy kernel launch failed")
             return
+        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "tight":  # A/B: relaxed polls, no sleep
+            import ctypes
+            self.lib.gate_arm_tight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+            if self.lib.gate_arm_tight(self.h, self.d, stream, 200_000) != 0:
+                raise RuntimeError("launch gate: kernel launch failed")
+            return
         if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "wait":  # A/B: stream wait on the flag
             import ctypes
             self.lib.gate_arm_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]

@@ -22,6 +22,14 @@ __global__ void __launch_bounds__(64) gate_kernel(const unsigned *flag, unsigned
   }
 }
 
+// Tight variant (A/B): relaxed system-scope loads (no cache invalidate per poll), no sleep.
+__global__ void __launch_bounds__(64) gate_tight_kernel(const unsigned *flag, unsigned long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u)
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+}
+
 // Busy variant (A/B): every workgroup keeps its CU issuing ALU work while the gate is
 // closed (so the clocks do not settle down during the host's enqueue); workgroup 0's
 // first lane polls the host flag and raises a device flag the others watch.
@@ -47,6 +55,13 @@ __global__ void __launch_bounds__(64) gate_busy_kernel(const unsigned *flag, uns
 }  // namespace
 
 extern "C" {
+
+int gate_arm_tight(unsigned *host_ptr, const unsigned *dev_ptr, void *stream, unsigned max_us) {
+  __atomic_store_n(host_ptr, 0u, __ATOMIC_SEQ_CST);
+  hipLaunchKernelGGL(gate_tight_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dev_ptr,
+                     (unsigned long long)max_us * 100ull);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // Busy gate on `stream`: `nwg` one-wave workgroups; dflag is a device word (cleared here).
 int gate_arm_busy(unsigned *host_ptr, const unsigned *dev_ptr, unsigned *dflag, void *stream, unsigned max_us,
