@@ -433,7 +433,7 @@ def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None, r
     return r
 
 
-def stream_h2d(efs, tables, device, n_frames=2048, n_cold=1000, n_paced=1000):
+def stream_h2d(efs, tables, device, n_frames=2048, n_cold=1000, n_paced=1000, sync=None):
     """BASELINE config 5 on this rank's GPU through the native stream group
     (mh_stream_group_*, one member here; N members round-robin frames over N GPUs):
     frames start in pinned host memory; each is copied H2D (codes + block offsets, one
@@ -464,6 +464,8 @@ def stream_h2d(efs, tables, device, n_frames=2048, n_cold=1000, n_paced=1000):
     t0 = time.perf_counter()
     run(n_cold, 1)
     cold_wall = time.perf_counter() - t0
+    if sync is not None:  # multi-rank: every rank's sustained phase starts together
+        sync()
     t0 = time.perf_counter()
     run(n_frames)
     wall = time.perf_counter() - t0
@@ -892,6 +894,38 @@ def main(argv=None) -> int:
             extras["hbm_probe"] = dict(ACHIEVABLE)
         extras["stream_h2d"] = stream_h2d(efs, tables, dev)  # config 5, one GPU
         extras["encode"] = encode_rate(dev, bb)
+        result["extras"] = extras
+
+    if world > 1 and not args.no_extras:
+        # The other multi-GPU configs on the same ranks (BASELINE configs[3], configs[4]):
+        # config 4 = 64 frames per launch per GPU, timed like the headline (barrier +
+        # synchronize, max over ranks); config 5 = every rank streaming host-resident
+        # frames through its own mh_stream at once, so the node's shared host PCIe and
+        # memory bandwidth is in the measurement.
+        extras = {}
+        b = batch_workload(args.batch)
+        nver = b.verify()
+        bsteps = 64
+        bwall, breg, bkms = b.run(bsteps, 16, use_graph=not args.no_graph, world=world)
+        extras["config4"] = {
+            "frames_per_launch_per_gpu": int(b.launches[0].n_frames), "frames_total": world * int(b.launches[0].n_frames),
+            "steps": bsteps, "value_MBps": round(world * b.pixels / (bwall / bsteps) / 1e6, 1),
+            "ms_per_step": round(bwall / bsteps * 1e3, 4), "frames_verified_rank0": nver,
+            "roofline_rank0": roofline(b.bytes, breg, bsteps, bkms, "batch", b.read_bytes, b.kernel_ms)}
+        del b
+        st = stream_h2d(efs, tables, dev, sync=dist.barrier)
+        got = [None] * world
+        dist.all_gather_object(got, {k: st[k] for k in ("fps", "h2d_GBps", "latency_us_p99", "latency_us_max",
+                                                        "cold_fps")})
+        extras["stream_h2d_all_ranks"] = {
+            "ranks": world, "fps_sum": round(sum(g["fps"] for g in got), 1),
+            "fps_min_rank": round(min(g["fps"] for g in got), 1),
+            "value_MBps_incl_pcie": round(sum(g["fps"] for g in got) * bb.size / 1e6, 1),
+            "h2d_GBps_sum": round(sum(g["h2d_GBps"] for g in got), 2),
+            "cold_fps_min_rank": round(min(g["cold_fps"] for g in got), 1),
+            "paced_latency_us_p99_max_rank": max(g["latency_us_p99"] for g in got),
+            "paced_latency_us_max": max(g["latency_us_max"] for g in got),
+            "method": "each rank: native mh_stream (2 slots), sustained phase started together after a barrier"}
         result["extras"] = extras
 
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
