@@ -152,7 +152,8 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     uint64_t v = q;
     if (delta) {
       // previous pixel: the last pixel of the row above in the same block, 0 for row 0
-      const uint32_t up = (uint32_t)__shfl_up((uint32_t)(q >> 56), 1);
+      // DPP row_shr:1 (lane - 1 inside each row of 16; r == 0 lanes ignore it)
+      const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(q >> 56), 0x111, 0xF, 0xF, false);
       const uint64_t p = (q << 8) | (r ? up : 0u);
       constexpr uint64_t kH = 0x8080808080808080ull;
       v = ((q | kH) - (p & ~kH)) ^ ((q ^ ~p) & kH);  // bytewise q - p
@@ -864,7 +865,7 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const 
     }
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      acc[m] += __shfl_xor(acc[m], 32);
+      acc[m] += xor_partner<32>(lane, acc[m]);
       if (lane < 32) s_cnt[wave][8 * q4 + m] = acc[m];
     }
   }
