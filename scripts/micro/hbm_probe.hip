@@ -4,7 +4,8 @@
 //   mode 0 copy (read N, write N), 1 read-only, 2 write-only,
 //   mode 3 the decoder's mix: read 2 vectors, write 3 (2.12 MB read : 3.15 MB written per
 //          2048x1536 frame is 0.67; 2:3 is the nearest whole-vector ratio);
-//   modes 4-6: copy, write-only and the mix with default-policy (not nt) stores.
+//   modes 4-6: copy, write-only and the mix with default-policy (not nt) stores;
+//   modes 7-8: write-only and the mix with 8-byte nt stores (the decoder's store width).
 // Loads are non-temporal too. Each mode reports the best of grids of 2, 4 and 16
 // workgroups per CU (scripts/micro/hbm_sweep.hip: the mix peaks at 2-4 per CU).
 // Built by metalhuffman_amd.build.build_probe() into scripts/micro/libhbm_probe.so.
@@ -46,12 +47,40 @@ __global__ void __launch_bounds__(256) stream_kernel(const v4u *__restrict__ src
   if (kMode == 1 && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = 1;
 }
 
+// 8-byte stores (the decoder's row stores: 64 lanes x 8 B = 512 contiguous bytes per
+// wave instruction), non-temporal: mode 7 write-only, mode 8 the 2:3 mix (16-B loads).
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+template <int kMode>
+__global__ void __launch_bounds__(256) stream8_kernel(const v4u *__restrict__ src, v2u *__restrict__ dst,
+                                                      size_t n_units) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_units; i += stride) {
+    if (kMode == 7) {
+      v2u v = {(unsigned)i, 1u};
+      __builtin_nontemporal_store(v, &dst[2 * i - (i % blockDim.x)]);           // two 512-B halves
+      __builtin_nontemporal_store(v, &dst[2 * i - (i % blockDim.x) + blockDim.x]);
+    } else {  // 2 x 16 B read, 6 x 8 B written per unit, each stream coalesced
+      const v4u a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[n_units + i]);
+      const size_t o = 2 * i - (i % blockDim.x);
+      const v2u w0 = {a.x, a.y}, w1 = {a.z, a.w}, w2 = {b.x, b.y}, w3 = {b.z, b.w};
+      __builtin_nontemporal_store(w0, &dst[o]);
+      __builtin_nontemporal_store(w1, &dst[o + blockDim.x]);
+      __builtin_nontemporal_store(w2, &dst[2 * n_units + o]);
+      __builtin_nontemporal_store(w3, &dst[2 * n_units + o + blockDim.x]);
+      __builtin_nontemporal_store(w0 ^ w2, &dst[4 * n_units + o]);
+      __builtin_nontemporal_store(w1 ^ w3, &dst[4 * n_units + o + blockDim.x]);
+    }
+  }
+}
+
 extern "C" {
 
 // Best-of-reps bandwidth in GB/s (bytes read + written) over `bytes` of traffic.
 // Returns 0 on success.
 int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
-  if (mode < 0 || mode > 6 || !gbps || reps < 1) return -1;
+  if (mode < 0 || mode > 8 || !gbps || reps < 1) return -1;
+  const int mode8 = mode >= 7 ? mode : 0;  // 8-byte-store variants
+  if (mode8) mode = mode8 == 7 ? 2 : 3;
   const bool nt = mode < 4;
   if (!nt) mode = mode == 4 ? 0 : mode == 5 ? 2 : 3;
   const size_t unit_bytes = mode == 3 ? 5 * 16 : mode == 0 ? 32 : 16;
@@ -77,7 +106,9 @@ int hbm_probe(int mode, size_t bytes, int reps, double *gbps) {
     (void)hipEventRecord(e0, 0);
     const v4u *s = (const v4u *)src;
     v4u *d = (v4u *)dst;
-    switch (mode + (nt ? 0 : 10)) {
+    if (mode8 == 7) hipLaunchKernelGGL(stream8_kernel<7>, grid, block, 0, 0, s, (v2u *)dst, n_units);
+    else if (mode8 == 8) hipLaunchKernelGGL(stream8_kernel<8>, grid, block, 0, 0, s, (v2u *)dst, n_units);
+    else switch (mode + (nt ? 0 : 10)) {
       case 0: hipLaunchKernelGGL(stream_kernel<0>, grid, block, 0, 0, s, d, n_units, sink); break;
       case 1: hipLaunchKernelGGL(stream_kernel<1>, grid, block, 0, 0, s, d, n_units, sink); break;
       case 2: hipLaunchKernelGGL(stream_kernel<2>, grid, block, 0, 0, s, d, n_units, sink); break;
