@@ -40,6 +40,22 @@ if GATE.ok():
         torch.cuda.synchronize()
         print(f"gated async encode {1e6 * (time.perf_counter() - t0) / reps:.1f} us/frame")
 
+# the same encodes captured once in a hipGraph and replayed (launch path of a
+# GPU-resident producer that re-encodes frames of one size)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    for k in range(64):
+        enc.encode_async(imgs[k % 4], codes=codes[k % 4])
+g.replay()
+torch.cuda.synchronize()
+for rep in range(2):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"graph replay encode {e0.elapsed_time(e1) * 1e3 / 64:.1f} us/frame")
+
 if len(sys.argv) > 2 and sys.argv[2] == "stamps":
     # library built with -DMH_TREE_STAMPS=1: s_memtime at the tree kernel's phase
     # boundaries in meta[2..10] (either path: the tree runs in enc_tree_kernel or workgroup 0)
