@@ -15,6 +15,7 @@ import sys
 root = sys.argv[1]
 res = {}
 kernels = {}
+enc = {}
 for d in sorted(glob.glob(os.path.join(root, "*_*_SIZE"))):
     base = os.path.basename(d)
     ctr = "FETCH_SIZE" if base.endswith("FETCH_SIZE") else "WRITE_SIZE"
@@ -23,7 +24,13 @@ for d in sorted(glob.glob(os.path.join(root, "*_*_SIZE"))):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            if ("mh_decode_kernel" in kn or "mh_decode_small_kernel" in kn) and r["Counter_Name"] == ctr:
+            if r["Counter_Name"] != ctr:
+                continue
+            if wl == "encode":  # per kernel of the encoder
+                for k in ("enc_split_kernel", "enc_code_kernel"):
+                    if k in kn:
+                        enc.setdefault(k, {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
+            elif "mh_decode_kernel" in kn or "mh_decode_small_kernel" in kn:
                 vals.append(float(r["Counter_Value"]))
                 kernels[wl] = "mh_decode_small_kernel" if "small" in kn else "mh_decode_kernel"
     if vals:
@@ -35,6 +42,14 @@ for wl, v in res.items():
         out[wl] = {"fetch_bytes_x2": round(2 * v["FETCH_SIZE"]), "write_bytes": round(v["WRITE_SIZE"]),
                    "traffic_bytes": round(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]),
                    "dispatches": v["dispatches"], "kernel": kernels[wl]}
-print(json.dumps({"per_launch_median": out,
+encode = {}
+for k, v in enc.items():
+    if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        f, w = statistics.median(v["FETCH_SIZE"]) * 1024.0, statistics.median(v["WRITE_SIZE"]) * 1024.0
+        encode[k] = {"fetch_bytes_x2": round(2 * f), "write_bytes": round(w), "traffic_bytes": round(2 * f + w),
+                     "dispatches": len(v["FETCH_SIZE"])}
+if encode:
+    encode["frame"] = "2048x1536 BigBridge block shuffle (scripts/enc_profile.py)"
+print(json.dumps({"per_launch_median": out, "encoder_per_launch_median": encode,
                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950)"},
                  indent=1))
