@@ -114,6 +114,43 @@ constexpr uint32_t kSplitBatch = MH_SPLIT_BATCH;
 #define MH_TREE_STAMPS 0
 #endif
 
+// Row r (8 pixels, little-endian in a u64) of 8x8 block b, zero past the frame edge
+// (Util.m:256-318: zero-filled blocks, row-major inside a block).
+__device__ __forceinline__ uint64_t block_row(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw,
+                                              uint64_t nb, uint32_t vec, uint64_t b, uint32_t r) {
+  if (b >= nb) return 0;
+  const uint32_t bx = (uint32_t)(b % bw), y = (uint32_t)(b / bw) * 8 + r;
+  if (y >= H) return 0;
+  const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
+  if (vec) return *reinterpret_cast<const uint64_t *>(row);  // W % 8 == 0, 8-byte aligned frame
+  uint64_t q = 0;
+  for (uint32_t c = 0; c < 8; ++c)
+    if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
+  return q;
+}
+
+// The 8 symbols of a block row from its pixels q (lane = 8 * block + r, all lanes
+// converged): per-block deltas (AAPLRenderer.m:432-515) in SWAR, the previous pixel of
+// row r > 0 being the last pixel of row r - 1, taken from the lane below by DPP
+// row_shr:1 (row 0's first delta is against 0); with the init byte
+// (AAPLRenderer.m:449-473) the block's first delta moves out and its symbol is 0.
+__device__ __forceinline__ uint64_t row_symbols(uint64_t q, uint32_t r, bool delta, bool init_byte,
+                                                uint32_t *first) {
+  uint64_t v = q;
+  *first = 0;
+  if (delta) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(q >> 56), 0x111, 0xF, 0xF, false);
+    const uint64_t p = (q << 8) | (r ? up : 0u);
+    constexpr uint64_t kH = 0x8080808080808080ull;
+    v = ((q | kH) - (p & ~kH)) ^ ((q ^ ~p) & kH);  // bytewise q - p
+    if (init_byte && r == 0) {
+      *first = (uint32_t)v & 0xFFu;
+      v &= ~0xFFull;
+    }
+  }
+  return v;
+}
+
 // Tiled mode (tile_hist != null, the fused path): workgroup t owns the kCodeTile
 // blocks of tile t (kCodeTile / 32 consecutive groups, loaded at once), stores the
 // tile's symbol counts in tile_hist[t] and re-arms the code kernel's table flag.
@@ -134,38 +171,18 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
   // one block row (8 pixels) of group g, zero past the frame edge
   auto load_row = [&](uint64_t g) -> uint64_t {
-    const uint64_t b = g * 32 + (threadIdx.x >> 3);
-    if (b >= nb) return 0;
-    const uint32_t bx = (uint32_t)(b % bw), y = (uint32_t)(b / bw) * 8 + r;
-    if (y >= H) return 0;
-    const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
-    if (vec) return *reinterpret_cast<const uint64_t *>(row);  // W % 8 == 0, 8-byte aligned frame
-    uint64_t q = 0;
-    for (uint32_t c = 0; c < 8; ++c)
-      if (bx * 8u + c < W) q |= (uint64_t)row[c] << (8 * c);
-    return q;
+    return block_row(gray, W, H, bw, nb, vec, g * 32 + (threadIdx.x >> 3), r);
   };
-  // one group of 32 blocks: deltas, init bytes, symbols out, histogram
+  // one group of 32 blocks: deltas, init bytes, symbols out (four-kernel path; the
+  // fused path's packer re-derives them from the pixels), histogram
   auto process = [&](uint64_t g, uint64_t q) {
     const uint64_t b = g * 32 + (threadIdx.x >> 3);
     const bool on = b < nb;
-    uint64_t v = q;
-    if (delta) {
-      // previous pixel: the last pixel of the row above in the same block, 0 for row 0
-      // DPP row_shr:1 (lane - 1 inside each row of 16; r == 0 lanes ignore it)
-      const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(q >> 56), 0x111, 0xF, 0xF, false);
-      const uint64_t p = (q << 8) | (r ? up : 0u);
-      constexpr uint64_t kH = 0x8080808080808080ull;
-      v = ((q | kH) - (p & ~kH)) ^ ((q ^ ~p) & kH);  // bytewise q - p
-      if (block_init && r == 0 && on) {
-        block_init[b] = (uint8_t)v;
-        v &= ~0xFFull;
-      }
-    } else if (block_init && r == 0 && on) {
-      block_init[b] = 0;
-    }
+    uint32_t first;
+    const uint64_t v = row_symbols(q, r, delta, block_init != nullptr, &first);
+    if (block_init && r == 0 && on) block_init[b] = (uint8_t)first;
     if (on) {
-      reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
+      if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
     }
   };
@@ -818,7 +835,13 @@ __device__ __forceinline__ void or_bits(uint32_t *lw, uint32_t pos, uint64_t v, 
   if (s + L > 64u) atomicOr(&lw[w + 2], bswap32((uint32_t)(a << (32u - s))));
 }
 
-__device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const uint16_t *tile_hist,
+struct Pixels {  // the frame as the split reads it
+  const uint8_t *gray;
+  uint32_t W, H, bw, vec;
+  bool delta, init_byte;
+};
+
+__device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uint16_t *tile_hist,
                                           const uint32_t *table, uint64_t *meta, uint64_t nb, uint32_t ntiles,
                                           uint32_t *offsets, uint32_t *words, int32_t *status) {
   __shared__ uint32_t tab[256];
@@ -830,10 +853,11 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const 
   MH_CODE_STAMP(t + 1, 0)
   const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
   const bool on = b < nb;
-  // this lane's 8 symbols and (lanes 0-7, t > 0) the previous block's: in flight
-  // while workgroup 0 builds the tree
-  const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
-  const uint64_t qp = (t > 0 && tid < 8) ? reinterpret_cast<const uint64_t *>(sym + (b0 - 1) * 64)[tid] : 0ull;
+  // this lane's 8 pixels (row `part` of its block) and (lanes 0-7, t > 0) the previous
+  // block's rows, in flight while workgroup 0 builds the tree; the symbols are the
+  // split's, re-derived here instead of going through a block-symbol buffer
+  const uint64_t gq = block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b, part);
+  const uint64_t gp = (t > 0 && tid < 8) ? block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
   {
     // counts of every symbol over tiles [0, t): 16-byte quad q (bins 8q..8q+7) of every
     // 32nd tile, eight loads in flight per lane (a late tile sums ~400 rows);
@@ -869,6 +893,10 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const 
       if (lane < 32) s_cnt[wave][8 * q4 + m] = acc[m];
     }
   }
+  // (every lane runs both: the DPP reads its neighbour; blocks past nb have zero pixels)
+  uint32_t first_unused;
+  const uint64_t q = row_symbols(gq, part, px.delta, px.init_byte, &first_unused);
+  const uint64_t qp = row_symbols(gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // used by lanes 0-7 of wave 0
   if (tid == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t f;
@@ -982,7 +1010,7 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const uint8_t *sym, const 
 __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kernel(uint64_t *hist, uint8_t *canon_out, uint32_t *table,
                                                                 uint64_t *meta, uint64_t *codes_len_out,
                                                                 uint64_t codes_cap, int32_t *status,
-                                                                const uint8_t *sym, const uint16_t *tile_hist,
+                                                                const Pixels px, const uint16_t *tile_hist,
                                                                 uint64_t nb, uint32_t ntiles, uint32_t *offsets,
                                                                 uint32_t *words) {
   static_assert(kTreeThreads == kCodeThreads, "workgroup 0 runs the tree");
@@ -995,7 +1023,7 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kern
     MH_CODE_STAMP(0, 3)
     return;
   }
-  pack_tile(blockIdx.x - 1, sym, tile_hist, table, meta, nb, ntiles, offsets, words, status);
+  pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, status);
 }
 
 }  // namespace
@@ -1073,9 +1101,10 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   if (ncode <= MH_FUSED_MAX_TILES && !four_kernel_path()) {
     // two launches: the tiled split, then tree + offsets + packing in one kernel
     hipLaunchKernelGGL(enc_split_kernel, dim3((uint32_t)ncode), dim3(256), 0, s, d_gray, width, height, bw, nb,
-                       flags, vec, w.sym, d_block_init, w.hist, w.tile_hist, w.meta);
+                       flags, vec, nullptr, d_block_init, w.hist, w.tile_hist, w.meta);
+    const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
     hipLaunchKernelGGL(enc_code_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist,
-                       d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, w.sym, w.tile_hist, nb,
+                       d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, px, w.tile_hist, nb,
                        (uint32_t)ncode, d_block_offsets, reinterpret_cast<uint32_t *>(d_codes));
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
