@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/traffic
 rm -rf $OUT; mkdir -p $OUT
-for wl in ${WLS:-frame batch tile8192 tile8192_random}; do
+for wl in ${WLS-frame batch tile8192 tile8192_random}; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d $OUT/${wl}_$ctr -o run -- \
       python3 bench.py --workload $wl --steps 20 --warmup 2 --no-extras --no-cpu-baseline --no-graph \
