@@ -3,7 +3,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out
+OUT=${OUT:-$GRAFT_REPO_ROOT/gpurun_out}
+mkdir -p $OUT
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 B="python3 bench.py --workload ${WL:-batch} --steps 10 --warmup 2 --no-extras --no-cpu-baseline"
 i=0
