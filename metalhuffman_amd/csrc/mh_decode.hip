@@ -79,6 +79,9 @@ namespace {
 #ifndef MH_LUT_FIRST            // 1: batch kernel issues the table's loads before the first header (A/B)
 #define MH_LUT_FIRST 0
 #endif
+#ifndef MH_EARLY_BARRIER        // 1 (with MH_LUT_FIRST): the table barrier right after the table's
+#define MH_EARLY_BARRIER 0      //    LDS stores, before any wave waits for its own first header
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -552,6 +555,14 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier that orders LDS only: the fences name the local address space,
+// so outstanding global loads (a wave's first header) are not waited for.
+[[maybe_unused]] __device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Oversize tile: stage + decode lanes [0,32) then [32,64), each from its own span.
 template <bool kDelta, class Cfg>
 __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t, uint32_t lane,
@@ -639,6 +650,11 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
 #pragma unroll
     for (uint32_t k = 0; k < kLutPer; ++k)
       if (threadIdx.x + k * blockDim.x < kLutChunks) dstv[threadIdx.x + k * blockDim.x] = L[k];
+#if MH_EARLY_BARRIER
+    // Only the table's LDS stores are fenced: the waves' first headers stay in flight,
+    // so no wave waits here for another wave's HBM round trip.
+    lds_barrier();
+#endif
   } else {
     hdr_issue(a, t0, lane, hc);
     if (a.lut) {
@@ -666,7 +682,11 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   hdr_issue(a, next_tile(t0), lane, hn);
 
   if (a.lut) {
+#if MH_LUT_FIRST && MH_EARLY_BARRIER
+    if (!lut_regs) __syncthreads();
+#else
     __syncthreads();
+#endif
   } else {
     build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
