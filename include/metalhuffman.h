@@ -72,6 +72,16 @@ extern "C" {
                                     its middle bit, re-synchronised through
                                     ds_bpermute; same output. Ignored by batch
                                     launches */
+#define MH_FLAG_ANY_ORDER 0x4u   /* the launch may start before earlier work on
+                                    the stream has finished (the AQL dispatch packet
+                                    goes out without its barrier bit, HIP's
+                                    hipExtAnyOrderLaunch). The caller guarantees that
+                                    nothing still running on the stream writes this
+                                    call's inputs or touches its output -- e.g. a run
+                                    of decodes of resident frames into distinct
+                                    rasters, the first of them launched without the
+                                    flag. Later work on the stream still waits for it.
+                                    Same output */
 
 /* Shared/HuffmanLookupSymbol.h:7-10: 2-byte entry. In T1, bitWidth == 0 marks
  * an escape whose `symbol` is the T2 subtable index (HuffmanUtil.cpp:639-646). */

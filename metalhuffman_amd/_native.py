@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("MH_LIB") or os.path.join(_PKG, "libmetalhuffman_amd.s
 MH_OK = 0
 MH_FLAG_NO_DELTA = 0x1
 MH_FLAG_LANE_PAIRS = 0x2  # experimental lane-pair single-frame decode (A/B)
+MH_FLAG_ANY_ORDER = 0x4  # the launch may overlap earlier work on the stream (caller guarantees independence)
 MH_ENCODE_WORKSPACE_ZEROED = 0x100  # the encoder workspace was zero-filled once (mh_encode_frame_device*)
 MH_CODES_PAD = 4
 MH_TABLE2_MAX_ENTRIES = 257 * 256

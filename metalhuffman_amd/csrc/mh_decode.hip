@@ -21,6 +21,7 @@
 //     (AAPLShaders.metal:260-262) and stores each finished 8-pixel block row as one
 //     8-byte store: the 64 lanes of a wave write 512 contiguous bytes per row.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <stdint.h>
 
@@ -1198,8 +1199,18 @@ const DeviceInfo *device_info(hipStream_t s) {
   return d.cus ? &d : nullptr;
 }
 
+// One kernel launch; any_order (MH_FLAG_ANY_ORDER) clears the dispatch packet's
+// barrier bit so the kernel may start while earlier work on the stream drains.
+#define MH_LAUNCH(kernel, grid, block, s, any_order, arg)                                          \
+  do {                                                                                            \
+    if (any_order)                                                                                \
+      hipExtLaunchKernelGGL(kernel, grid, block, 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, arg); \
+    else                                                                                          \
+      hipLaunchKernelGGL(kernel, grid, block, 0, s, arg);                                         \
+  } while (0)
+
 template <bool kDelta>
-int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
+int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order) {
   DecodeArgs a = a0;
   const DeviceInfo *di = device_info(s);
   if (!di) return MH_ERR_HIP;
@@ -1210,7 +1221,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
     a.tiles_per_frame = (a.nb + 31u) / 32u;
     a.total_tiles = a.tiles_per_frame * n_frames;
     a.n_groups = (a.total_tiles + kLpWaves - 1) / kLpWaves;
-    hipLaunchKernelGGL(mh_decode_lanepair_kernel<kDelta>, dim3(a.n_groups), dim3(kLpWaves * 64), 0, s, a);
+    MH_LAUNCH(mh_decode_lanepair_kernel<kDelta>, dim3(a.n_groups), dim3(kLpWaves * 64), s, any_order, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
@@ -1218,7 +1229,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
     const uint32_t nw = kSmallWaves;
     a.n_groups = (a.total_tiles + nw - 1) / nw;
-    hipLaunchKernelGGL(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), 0, s, a);
+    MH_LAUNCH(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), s, any_order, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   // Waves per workgroup: spread a small launch (one 2048x1536 frame = 768 tiles)
@@ -1233,7 +1244,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs) {
   const uint32_t resident = (uint32_t)(cus * di->occ[kDelta ? 1 : 0][nw]);
 #endif
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
-  hipLaunchKernelGGL(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), 0, s, a);
+  MH_LAUNCH(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), s, any_order, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
@@ -1280,7 +1291,7 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (!fr || !d_out || !fr->d_block_offsets || !fr->d_codes || !fr->d_table1 || !fr->d_table2)
     return MH_ERR_INVALID_ARG;
   if (fr->n_frames == 0 || (fr->n_frames > 1 && !fr->d_frame_code_offsets)) return MH_ERR_INVALID_ARG;
-  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_LANE_PAIRS)) return MH_ERR_INVALID_ARG;
+  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_LANE_PAIRS | MH_FLAG_ANY_ORDER)) return MH_ERR_INVALID_ARG;
   const mh_dims &d = fr->dims;
   if (!d.width || !d.height || d.width > MH_MAX_DIM || d.height > MH_MAX_DIM ||
       d.block_width != (d.width + 7) / 8 || d.block_height != (d.height + 7) / 8)
@@ -1323,7 +1334,8 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   a.total_tiles = (uint32_t)total;
   hipStream_t s = (hipStream_t)stream;
   const bool lp = (fr->flags & MH_FLAG_LANE_PAIRS) != 0;
-  return (fr->flags & MH_FLAG_NO_DELTA) ? launch<false>(a, s, lp) : launch<true>(a, s, lp);
+  const bool ao = (fr->flags & MH_FLAG_ANY_ORDER) != 0;
+  return (fr->flags & MH_FLAG_NO_DELTA) ? launch<false>(a, s, lp, ao) : launch<true>(a, s, lp, ao);
 }
 
 }  // extern "C"

@@ -170,7 +170,7 @@ def _frame_struct(frames: DeviceFrames, tables: DeviceTables) -> N.mh_frame:
 def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tensor] = None,
            stream: Optional[torch.cuda.Stream] = None, extra_flags: int = 0) -> torch.Tensor:
     """Decode every frame into out[n, H, pitch] (pitch = W rounded up to 8).
-    extra_flags: decode-only flags ORed into the frame's (MH_FLAG_LANE_PAIRS)."""
+    extra_flags: decode-only flags ORed into the frame's (MH_FLAG_LANE_PAIRS, MH_FLAG_ANY_ORDER)."""
     dev = frames.codes.device
     if tables.table1.device != dev:
         raise ValueError("tables and frames must live on the same device")

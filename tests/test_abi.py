@@ -68,6 +68,7 @@ def _frame(**kw):
 @pytest.mark.parametrize("kw,status", [
     (dict(d_codes=None), -1),
     (dict(flags=0x80), -1),
+    (dict(flags=0x8), -1),                                     # first unassigned flag bit
     (dict(n_frames=0), -1),
     (dict(n_frames=2), -1),                                    # batch without frame offsets
     (dict(table2_entries=100), -5),

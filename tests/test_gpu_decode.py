@@ -379,3 +379,33 @@ def test_config4_full_shard_one_launch(mh, oracle, device, bigbridge):
     assert not bad, bad
     for i in (0, 41):
         assert np.array_equal(out[i, :, :2048].cpu().numpy(), _oracle_decode(oracle, efs[i])), i
+
+
+@pytest.mark.parametrize("lane_pairs", [False, True])
+def test_any_order_run_of_frames(mh, oracle, device, bigbridge, lane_pairs):
+    """MH_FLAG_ANY_ORDER: a run of one-frame launches on one stream, every launch after
+    the first without the dispatch barrier (it may start while the previous decode
+    drains), each into its own raster -- the bench's timed region. Then a launch WITHOUT
+    the flag reuses frame 0's raster for another frame: stream order still holds for it.
+    Every raster equals its input; frame 3 also equals the oracle's decode."""
+    import torch
+    from metalhuffman_amd import _native as N
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import frames as F
+    imgs = [F.block_shuffle(bigbridge, 7000 + s) for s in range(12)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    frs = [D.DeviceFrames.pack([ef], device) for ef in efs]
+    outs = [torch.full((1, 1536, 2048), 0xA5, dtype=torch.uint8, device=device) for _ in efs]
+    extra = N.MH_FLAG_LANE_PAIRS if lane_pairs else 0
+    for rep in range(3):
+        for i, fr in enumerate(frs[:-1]):
+            D.decode(fr, tabs, outs[i], extra_flags=extra | (N.MH_FLAG_ANY_ORDER if i else 0))
+    D.decode(frs[-1], tabs, outs[0], extra_flags=extra)  # barrier launch: after every earlier one
+    torch.cuda.synchronize(device)
+    ref = torch.from_numpy(np.stack(imgs)).to(device)
+    assert torch.equal(outs[0][0], ref[-1])
+    bad = [i for i in range(1, len(efs) - 1) if not torch.equal(outs[i][0], ref[i])]
+    assert not bad, bad
+    assert np.array_equal(outs[3][0].cpu().numpy(), _oracle_decode(oracle, efs[3]))
