@@ -87,9 +87,9 @@ DECODE_FLAGS = int(os.environ.get("MH_BENCH_DECODE_FLAGS", "0"), 0)
 # MH_BENCH_ANY_ORDER=1: inside an eager timed region every launch after the first goes
 # out with MH_FLAG_ANY_ORDER (no barrier bit: it may start while the previous frame's
 # decode drains; each launch writes its own raster). The first launch keeps the
-# barrier, so nothing starts before the region opens.
-# Measured: 5.56-5.62 vs 5.78-5.82 us per launch over 20/64-launch regions
-# (profiles/r02_v19_any_order_ab.txt).
+# barrier, so nothing starts before the region opens. On gfx950 the dispatches do not
+# overlap (scripts/micro/any_order_probe.hip); the gap between them shrinks: 5.56-5.62
+# vs 5.78-5.82 us per launch over 20/64-launch regions (profiles/r02_v19_any_order_ab.txt).
 ANY_ORDER = os.environ.get("MH_BENCH_ANY_ORDER", "1") == "1"
 MH_FLAG_ANY_ORDER = 0x4
 

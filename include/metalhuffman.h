@@ -81,7 +81,10 @@ extern "C" {
                                     of decodes of resident frames into distinct
                                     rasters, the first of them launched without the
                                     flag. Later work on the stream still waits for it.
-                                    Same output */
+                                    Same output. On gfx950 the dispatches still run
+                                    one after another (scripts/micro/any_order_probe
+                                    .hip); the flag trims ~0.1-0.2 us of the gap
+                                    between them */
 
 /* Shared/HuffmanLookupSymbol.h:7-10: 2-byte entry. In T1, bitWidth == 0 marks
  * an escape whose `symbol` is the T2 subtable index (HuffmanUtil.cpp:639-646). */
