@@ -262,12 +262,33 @@ __device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
   key = take ? p : key;
 }
 
-// ... on 32-bit keys (frames of < 2^22 symbols, see tree_body)
+// ... on 32-bit keys (frames of < 2^22 symbols, see tree_body). Keys are distinct, so
+// the lower lane keeps min(key, partner) and the upper one the max: v_min / v_max and
+// one select on a lane-constant mask (no compare -> VCC -> select chain). The swap
+// stages (D = 32, 16) take min / max straight from the two permlane outputs: each lane
+// holds its own key in one and its partner's in the other.
+#ifndef MH_TREE_MINMAX
+#define MH_TREE_MINMAX 1
+#endif
 template <uint32_t D>
 __device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
+#if MH_TREE_MINMAX
+  uint32_t a, b;
+  if constexpr (D == 32 || D == 16) {
+    const auto r = D == 32 ? __builtin_amdgcn_permlane32_swap(key, key, false, false)
+                           : __builtin_amdgcn_permlane16_swap(key, key, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    a = key;
+    b = xor_partner<D>(lane, key);
+  }
+  key = (lane & D) ? max(a, b) : min(a, b);
+#else
   const uint32_t p = xor_partner<D>(lane, key);
   const bool take = (p < key) != ((lane & D) != 0u);  // keys are distinct
   key = take ? p : key;
+#endif
 }
 
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
@@ -446,9 +467,12 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
       const uint32_t q = s_qv[lane], qid = s_qid[lane];
 #endif
       const uint32_t s0 = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_readlane(q, 1);
-      uint32_t k = (uint32_t)__popcll(__ballot((lane & 1u) && q <= s0));  // Q sorted: a prefix
+      // ballots of plain compares, masked on the scalar side (a ballot of a combined
+      // condition re-materialises it in a VGPR first)
+      uint32_t k = (uint32_t)__popcll(__ballot(q <= s0) & 0xAAAAAAAAAAAAAAAAull);  // odd lanes; Q sorted: a prefix
       k = min(k, n - 1 - m);
-      const uint32_t nl = (uint32_t)__popcll(__ballot(lane < 2 * k && qid < n));
+      const uint64_t first2k = 2 * k >= 64 ? ~0ull : (1ull << (2 * k)) - 1ull;
+      const uint32_t nl = (uint32_t)__popcll(__ballot(qid < n) & first2k);
 #if MH_TREE_BITONIC
       // pair j = lanes (2j, 2j+1): the odd lane adds its even neighbour (DPP) and
       // appends the new node; both lanes point their node at it
