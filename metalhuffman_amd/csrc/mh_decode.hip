@@ -80,12 +80,6 @@ namespace {
 #ifndef MH_LUT_FIRST            // 1: batch kernel issues the table's loads before the first header (A/B)
 #define MH_LUT_FIRST 0
 #endif
-#ifndef MH_LUT_BANK_SWIZZLE     // 1: the batch kernel's LDS copy of the 13-bit first level is stored
-#define MH_LUT_BANK_SWIZZLE 0   //    with dword d at d ^ ((d >> 5) & 31) (bank XOR row)
-#endif
-#ifndef MH_EARLY_BARRIER        // 1 (with MH_LUT_FIRST): the table barrier right after the table's
-#define MH_EARLY_BARRIER 0      //    LDS stores, before any wave waits for its own first header
-#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -118,17 +112,6 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
   return __builtin_amdgcn_perm(0u, x, 0x00010203u);
 }
 
-// Bank swizzle of the first-level table in LDS (MH_LUT_BANK_SWIZZLE): dword d of the
-// table lives at d ^ ((d >> 5) & 31), i.e. its bank (d mod 32) is XORed with its row.
-// The window bits that pick the bank are the ones after the current code -- the next
-// codes, skewed towards the frequent short ones -- so lanes on different rows often
-// share a bank; XOR-ing the row in spreads them (modelled on BigBridge's bitstream:
-// 7.83 -> 6.88 LDS cycles per wave-gather, the 8192^2 tile 8.35 -> 6.82). Rows never
-// mix, so the second level (after the first 128 rows) keeps its layout.
-//   byte address of a u16 entry: a -> a ^ ((a >> 5) & 0x7C)
-//   entry index:                 p -> p ^ ((p >> 5) & 0x3E)
-__device__ __forceinline__ uint32_t lut_swz_entry(uint32_t p) { return p ^ ((p >> 5) & 0x3Eu); }
-
 // AAPLShaders.metal:159-170 / HuffmanUtil.cpp:961-995 on a 16-bit pattern.
 // Out-of-range T2 reads (corrupt tables only) return the all-zero entry.
 __device__ __forceinline__ uint32_t split_lookup(const uint16_t *t1, const uint16_t *t2,
@@ -152,16 +135,15 @@ __device__ __forceinline__ uint32_t split_lookup(const uint16_t *t1, const uint1
 //     of >= 4 patterns) occupy at most 128 prefixes from P0.
 //   L2[sub*8 + x] = step_word(split_lookup(((P0 + sub - 1) << 3) | x)), sub >= 1;
 //   L2 subtable 0 is all zero (escapes beyond the long-code range: invalid windows).
-template <bool kSwz, class SyncFn>
+template <class SyncFn>
 __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_entries,
                           uint16_t *lut, uint32_t *p0, uint32_t tid, uint32_t nthreads,
                           SyncFn sync) {
-  const auto l1 = [](uint32_t p) { return kSwz ? lut_swz_entry(p) : p; };
   if (tid == 0) *p0 = (uint32_t)kL1Entries;
   sync();
   for (uint32_t p = tid; p < (uint32_t)kL1Entries; p += nthreads) {
     const uint32_t e = split_lookup(t1, t2, t2_entries, p << kL2Bits);
-    lut[l1(p)] = (uint16_t)step_word(e);
+    lut[p] = (uint16_t)step_word(e);
     if ((e >> 8) > (uint32_t)kLutBits) atomicMin(p0, p);
   }
   for (uint32_t i = tid; i < (uint32_t)(kLutEntries - kL1Entries); i += nthreads)
@@ -170,7 +152,7 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
   const uint32_t P0 = *p0;
   for (uint32_t p = P0 + tid; p < (uint32_t)kL1Entries; p += nthreads) {
     const uint32_t sub = p - P0 + 1;
-    lut[l1(p)] = (uint16_t)(sub < (uint32_t)kL2Subtables ? sub : 0u);
+    lut[p] = (uint16_t)(sub < (uint32_t)kL2Subtables ? sub : 0u);
   }
   const uint32_t nl2 = ((uint32_t)kL1Entries - P0) << kL2Bits;
   for (uint32_t i = tid; i < nl2 && i < (uint32_t)(kL2Entries - (1 << kL2Bits)); i += nthreads)
@@ -250,11 +232,10 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 //   window the refill selects (two shifts in parallel), taking the word move off
 //   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
 template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits,
-          bool kSwizzle = false, bool kLutSwizzle = false>
+          bool kSwizzle = false>
 struct StepCfg {
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
-  static constexpr bool kLutSwz = kLutSwizzle;  // first level bank-swizzled (lut_swz_entry)
   static constexpr bool kSpec = kSpecRefill;
   static constexpr bool kMasked = kMaskedRefill && !kSpecRefill;
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
@@ -262,16 +243,14 @@ struct StepCfg {
   static constexpr uint32_t kRefillAt = kCur - 32u;           // low byte <= this: sh >= 32
 };
 
-using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, true, false,
-                     MH_LUT_BANK_SWIZZLE != 0>;  // the batch kernel's step
+using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  // the batch kernel's step
 // ... and its escape-free twin, for tables whose longest code is <= 13 bits (the
 // first level then decodes every window; no per-symbol escape test)
-using Lut13NoEsc = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false, false,
-                          MH_LUT_BANK_SWIZZLE != 0>;
+using Lut13NoEsc = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false>;
 // ... and for flat tables (every code the same length, e.g. uniform bytes: every
 // block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
 using Lut13Flat = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false,
-                          MH_STAGE_SWIZZLE != 0, MH_LUT_BANK_SWIZZLE != 0>;
+                          MH_STAGE_SWIZZLE != 0>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -304,12 +283,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_LOOKUP(A1)                                                               \
-  uint32_t e;                                                                       \
-  {                                                                                 \
-    const uint32_t a_ = (A1);                                                       \
-    e = *reinterpret_cast<const uint16_t *>(                                        \
-        lut + (MH_DIAG_BROADCAST_LUT ? 0u : Cfg::kLutSwz ? a_ ^ ((a_ >> 5) & 0x7Cu) : a_)); \
-  }
+  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? 0u : (A1)));
 #define MH_FINISH(J, OW)                                                            \
   {                                                                                 \
     if constexpr (Cfg::kEsc) {                                                      \
@@ -579,14 +553,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Workgroup barrier that orders LDS only: the fences name the local address space,
-// so outstanding global loads (a wave's first header) are not waited for.
-[[maybe_unused]] __device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 // Oversize tile: stage + decode lanes [0,32) then [32,64), each from its own span.
 template <bool kDelta, class Cfg>
 __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t, uint32_t lane,
@@ -633,21 +599,6 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
   (void)fbits;
 }
 
-// 16-byte chunk i of the prepared table -> its place in the batch kernel's LDS copy
-// (first level bank-swizzled under MH_LUT_BANK_SWIZZLE: a chunk's four dwords stay one
-// aligned chunk of the same row, permuted by XOR with the row's low two bits).
-__device__ __forceinline__ void lut_put_chunk(v4u32 *dst, uint32_t i, v4u32 v) {
-#if MH_LUT_BANK_SWIZZLE
-  if (i < (uint32_t)(kL1Entries * 2 / 16)) {
-    const uint32_t r = (i >> 3) & 31u;  // row (32 dwords = 8 chunks)
-    if (r & 1u) v = v.yxwz;
-    if (r & 2u) v = v.zwxy;
-    i ^= r >> 2;
-  }
-#endif
-  dst[i] = v;
-}
-
 // Persistent loop: wave w of workgroup g decodes tiles g*W + w, + gridDim*W, ...
 // Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
 // header of tile i+2 and the code span of tile i+1 are in flight into registers;
@@ -688,18 +639,13 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
 #pragma unroll
     for (uint32_t k = 0; k < kLutPer; ++k)
-      if (threadIdx.x + k * blockDim.x < kLutChunks) lut_put_chunk(dstv, threadIdx.x + k * blockDim.x, L[k]);
-#if MH_EARLY_BARRIER
-    // Only the table's LDS stores are fenced: the waves' first headers stay in flight,
-    // so no wave waits here for another wave's HBM round trip.
-    lds_barrier();
-#endif
+      if (threadIdx.x + k * blockDim.x < kLutChunks) dstv[threadIdx.x + k * blockDim.x] = L[k];
   } else {
     hdr_issue(a, t0, lane, hc);
     if (a.lut) {
       const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
       v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-      for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) lut_put_chunk(dstv, i, src[i]);
+      for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
     }
   }
 #else
@@ -709,7 +655,7 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   if (a.lut) {
     const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) lut_put_chunk(dstv, i, src[i]);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
   }
 #endif
 
@@ -721,14 +667,9 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   hdr_issue(a, next_tile(t0), lane, hn);
 
   if (a.lut) {
-#if MH_LUT_FIRST && MH_EARLY_BARRIER
-    if (!lut_regs) __syncthreads();
-#else
     __syncthreads();
-#endif
   } else {
-    build_lut<MH_LUT_BANK_SWIZZLE != 0>(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x,
-                                        [] { __syncthreads(); });
+    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
   }
   MH_STAMP(2);
   if (cur_staged) span_write<kSwz>(cur, lane, R, stage);
