@@ -270,6 +270,9 @@ __device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
 #ifndef MH_TREE_MINMAX
 #define MH_TREE_MINMAX 1
 #endif
+#ifndef MH_TREE_SORT_RANK  // 1: leaf ranks by wave bitonic sorts + binary search (32-bit keys)
+#define MH_TREE_SORT_RANK 1
+#endif
 template <uint32_t D>
 __device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
 #if MH_TREE_MINMAX
@@ -289,6 +292,34 @@ __device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
   const bool take = (p < key) != ((lane & D) != 0u);  // keys are distinct
   key = take ? p : key;
 #endif
+}
+
+// Ascending bitonic sort of one key per lane over the wave (21 compare-exchange stages
+// of size K, distance J; duplicates allowed): min / max plus one lane-constant select.
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ void sort_stage(uint32_t lane, uint32_t &key) {
+  uint32_t a, b;
+  if constexpr (J == 32 || J == 16) {  // each lane gets its own key in one output, its partner's in the other
+    const auto r = J == 32 ? __builtin_amdgcn_permlane32_swap(key, key, false, false)
+                           : __builtin_amdgcn_permlane16_swap(key, key, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    a = key;
+    b = xor_partner<J>(lane, key);
+  }
+  const bool up = K == 64 || (lane & K) == 0u;
+  key = (((lane & J) == 0u) == up) ? min(a, b) : max(a, b);
+}
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ void sort_merge(uint32_t lane, uint32_t &key) {
+  sort_stage<K, J>(lane, key);
+  if constexpr (J > 1) sort_merge<K, J / 2>(lane, key);
+}
+template <uint32_t K = 2>
+__device__ __forceinline__ void wave_sort64(uint32_t lane, uint32_t &key) {
+  sort_merge<K, K / 2>(lane, key);
+  if constexpr (K < 64) wave_sort64<K * 2>(lane, key);
 }
 
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
@@ -364,6 +395,37 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     const uint32_t ks = tid & 255u, part = tid >> 8;
     uint32_t below = 0, present;
     if (k32) {  // counts < 2^22: (count << 8 | symbol) fits 32 bits
+#if MH_TREE_SORT_RANK
+      // The four symbol waves sort their 64 keys in registers (bitonic), then thread
+      // (part, q) counts the keys of run `part` below sorted element q by binary search
+      // (7 dependent LDS reads); q's rank is the sum over the four runs.
+      uint32_t key = f ? (uint32_t)(f << 8) | tid : 0u;
+      present = (uint32_t)__syncthreads_count(f != 0);
+      if (sym_thread) {
+        wave_sort64(tid & 63u, key);
+        s_key32[tid] = key;
+      }
+      __syncthreads();
+      const uint32_t kq = s_key32[ks];
+      if (part == (ks >> 6)) {
+        below = ks & 63u;  // its place in its own run (present keys are distinct)
+      } else {
+        const uint32_t *run = s_key32 + 64u * part;
+#pragma unroll
+        for (uint32_t step = 64; step; step >>= 1)
+          if (below + step <= 64u && run[below + step - 1u] < kq) below += step;
+      }
+      s_below[part][ks] = below;
+      __syncthreads();
+      if (sym_thread) {
+        const uint32_t k = s_key32[tid];  // sorted element tid
+        if (k) {
+          const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
+          s_leaf_sym[rank] = k & 0xFFu;
+          s_lw[rank] = k >> 8;
+        }
+      }
+#else
       if (sym_thread) s_key32[tid] = f ? (uint32_t)(f << 8) | tid : 0u;
       present = (uint32_t)__syncthreads_count(f != 0);
       const uint32_t key = s_key32[ks];
@@ -373,6 +435,14 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
         const uint4 v = kv[t];
         below += (v.x < key ? 1u : 0u) + (v.y < key ? 1u : 0u) + (v.z < key ? 1u : 0u) + (v.w < key ? 1u : 0u);
       }
+      s_below[part][ks] = below;
+      __syncthreads();
+      if (sym_thread && f) {
+        const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
+        s_leaf_sym[rank] = tid;
+        s_lw[rank] = (uint32_t)f;
+      }
+#endif
     } else {
       if (sym_thread) s_key[tid] = f ? (f << 8) | tid : 0;
       present = (uint32_t)__syncthreads_count(f != 0);
@@ -384,13 +454,13 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
         below += v.x < key ? 1u : 0u;
         below += v.y < key ? 1u : 0u;
       }
-    }
-    s_below[part][ks] = below;
-    __syncthreads();
-    if (sym_thread && f) {
-      const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
-      s_leaf_sym[rank] = tid;
-      s_lw[rank] = (uint32_t)f;
+      s_below[part][ks] = below;
+      __syncthreads();
+      if (sym_thread && f) {
+        const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
+        s_leaf_sym[rank] = tid;
+        s_lw[rank] = (uint32_t)f;
+      }
     }
     if (tid == 0) s_n = present;
   }
