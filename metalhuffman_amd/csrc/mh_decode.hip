@@ -268,12 +268,18 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
                                              uint32_t prev, __amdgpu_buffer_rsrc_t out,
                                              uint32_t row0, uint32_t pitch, bool dead,
                                              uint32_t prio = 0) {
-  const uint8_t *wa = src.at((p >> 5) * 4u);
-  const auto rd = [&](const uint8_t *q) -> uint32_t {
+  // wa: LDS address of hi's word in the staged span. An explicit local-address-space
+  // pointer keeps its arithmetic 32-bit (a generic pointer was carried as a 64-bit value:
+  // one 64-bit add per refill) and lets the reads fold their constant offsets.
+  typedef const __attribute__((address_space(3))) uint8_t *lds_u8;
+  typedef const __attribute__((address_space(3))) uint32_t *lds_u32;
+  const lds_u8 base = (lds_u8)src.w;
+  lds_u8 wa = base + (p >> 5) * 4u;
+  const auto rd = [&](lds_u8 q) -> uint32_t {
     if constexpr (Cfg::kSwz)
-      return word_at(src.w + swz_off((uint32_t)(q - src.w)));
+      return *(lds_u32)(base + swz_off((uint32_t)(q - base)));
     else
-      return word_at(q);
+      return *(lds_u32)q;
   };
   uint32_t S = (prev << 8) + Cfg::kCur - (p & 31u);
   uint32_t hi = rd(wa);
