@@ -282,6 +282,11 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
       return *(lds_u32)q;
   };
   uint32_t S = (prev << 8) + Cfg::kCur - (p & 31u);
+  // An odd refill bound (the 14-bit table's) goes in as an opaque scalar: as a literal
+  // the compiler rewrites (S & 0xFF) <= K as (S & 0xFE) < K + 1, which no longer folds
+  // into a byte-select (SDWA) compare -- one more VALU on every refill step's chain.
+  uint32_t kRefill = Cfg::kRefillAt;
+  if constexpr ((Cfg::kRefillAt & 1u) != 0u) asm("s_mov_b32 %0, %1" : "=s"(kRefill) : "n"(Cfg::kRefillAt));
   uint32_t hi = rd(wa);
   uint32_t lo = rd(wa + 4);
   uint32_t nw = rd(wa + 8);
@@ -330,7 +335,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   }
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
-    const bool c = (S & 0xFFu) <= Cfg::kRefillAt;                                   \
+    const bool c = (S & 0xFFu) <= kRefill;                                         \
     if constexpr (Cfg::kSpec) {                                                     \
       const uint32_t v0 = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (S & 63u));  \
       const uint32_t v1 = (uint32_t)(((((uint64_t)lo) << 32) | nw) >> ((S + 32u) & 63u)); \
