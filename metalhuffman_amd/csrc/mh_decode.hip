@@ -413,6 +413,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base,
 
 // A tile's header loads (issued one tile ahead; all VMEM so that no scalar load
 // is pending in lgkmcnt while the decode waits on LDS reads).
+// tile -> frame. A launch of one frame skips the division (a uniform branch): the
+// division is ~30 instructions ahead of a wave's first HBM load (its block offsets).
+__device__ __forceinline__ uint32_t frame_of(const DecodeArgs &a, uint32_t tile) {
+  if (a.total_tiles <= a.tiles_per_frame) return 0u;
+  return tile / a.tiles_per_frame;
+}
+
 struct TileHdr {
   uint32_t tile;      // wave-uniform; >= total_tiles: no tile
   uint32_t off;       // this lane's block start bit
@@ -429,7 +436,7 @@ __device__ __forceinline__ void hdr_issue(const DecodeArgs &a, uint32_t tile, ui
   // compiler from waiting on the span prefetch to re-zero these registers.
   tile = __builtin_amdgcn_readfirstlane(tile);
   const bool live = tile < a.total_tiles;
-  const uint32_t f = live ? tile / a.tiles_per_frame : 0u;
+  const uint32_t f = live ? frame_of(a, tile) : 0u;
   const uint32_t b = (live ? (tile - f * a.tiles_per_frame) * 64u : 0u) + lane;
   h.tile = tile;
   const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(a.offsets + (uint64_t)f * a.nb, live ? a.nb * 4u : 0u);
@@ -464,7 +471,7 @@ struct Tile {
 __device__ __forceinline__ Tile hdr_resolve(const DecodeArgs &a, const TileHdr &h, uint32_t lane) {
   Tile t;
   t.tile = h.tile;
-  t.f = h.tile / a.tiles_per_frame;
+  t.f = frame_of(a, h.tile);
   t.b0 = (h.tile - t.f * a.tiles_per_frame) * 64u;
   const uint32_t b = t.b0 + lane;
   t.valid = b < a.nb;
