@@ -353,6 +353,9 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     }                                                                               \
   }
 
+  // dead lanes store at >= 2^31 + r * pitch: past every output descriptor's range
+  // (<= 0x7FFFFFF0 bytes), so the hardware drops them -- one select per tile, not per row
+  const uint32_t rbase = dead ? 0x80000000u : row0;
 #if MH_ROW_UNROLL == 8
 #pragma unroll
 #else
@@ -388,7 +391,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
       v2u32 v;
       v.x = o0;
       v.y = o1;
-      const uint32_t off = dead ? 0xFFFFFFF0u : row0 + r * pitch;
+      const uint32_t off = rbase + r * pitch;
       __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
     }
   }
