@@ -863,6 +863,8 @@ def main(argv=None) -> int:
         result["ungated_ms_per_step"] = round(wl.ungated_wall / args.steps * 1e3, 5)
         result["ungated_value"] = round(world * wl.pixels / (wl.ungated_wall / args.steps) / 1e6, 1)
     result["frames_verified"] = frames_verified
+    # the sources this library was built from (the loader refuses a stale library)
+    result["source_stamp"] = dict(B.source_stamps(), loaded=mh.lib().mh_build_stamp().decode()[:16])
     if ranks_ok is not None:
         result["ranks_verified"] = ranks_ok
     if t_bcast_us is not None:

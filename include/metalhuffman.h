@@ -372,6 +372,11 @@ int mh_build_single_table(const uint8_t canon_header[256], mh_lookup_symbol tabl
 /* Utilities */
 const char *mh_error_string(int status);
 int mh_device_count(void);
+/* sha256 (hex) over the compile flags, sources and headers the library was built
+ * from (metalhuffman_amd/build.py). The Python loader refuses a library whose
+ * stamp differs from the sources beside it; a debug build's self-check in the
+ * spirit of the renderer's DEBUG decode compare (AAPLRenderer.m:616-650). */
+const char *mh_build_stamp(void);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,7 @@ EXPORTS = (
     "mh_encode_frame_device_async",
     "mh_container_header", "mh_parse_container_header", "mh_check",
     "mh_decode_huffman_bits", "mh_decode_huffman_bits_from_tables", "mh_decode_frame_cpu",
+    "mh_build_stamp",
 )
 
 
@@ -84,6 +85,15 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} not found: build it with `python -m metalhuffman_amd.build` "
                 "(the HIP decoder has no fallback)")
         L = ctypes.CDLL(LIB_PATH)
+        L.mh_build_stamp.restype = ctypes.c_char_p
+        if not os.environ.get("MH_LIB"):  # experiment variants (MH_LIB) carry extra -D flags
+            from . import build as _build
+
+            want, have = _build.library_stamp(), L.mh_build_stamp().decode()
+            if have != want:
+                raise ImportError(
+                    f"{LIB_PATH} was built from other sources (stamp {have[:16]}, sources {want[:16]}): "
+                    "rebuild with `python -m metalhuffman_amd.build`")
         L.mh_decode.argtypes = [ctypes.POINTER(mh_frame), _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]
         L.mh_check.argtypes = [ctypes.POINTER(mh_frame), _vp, _vp]
         L.mh_lut_bytes.restype = ctypes.c_size_t

@@ -1,6 +1,6 @@
 """Phase timeline of one decode launch from a MH_DIAG_STAMPS=1 build (GPU, diagnostic).
 
-    MH_LIB=metalhuffman_amd/_variants/lib_diag.so python scripts/diag_stamps.py [--batch N]
+    MH_LIB=ab/lib_diag.so python scripts/diag_stamps.py [--batch N]
 
 Stamps (s_memrealtime, 100 MHz) per wave: 0 entry, 1 first header resolved,
 2 LUT ready, 3 first span staged, 4 first tile decoded (stores issued),

@@ -1,16 +1,16 @@
 # Encoder: parity, tree phase stamps, then per-kernel times of the default build and
-# of each variant in metalhuffman_amd/_variants (rocprofv3 kernel trace).
+# of each variant in ab (rocprofv3 kernel trace).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_encode.py > gpurun_out/enc_tests.log 2>&1 || { tail -30 gpurun_out/enc_tests.log; exit 1; }
 tail -1 gpurun_out/enc_tests.log
-if [ -f metalhuffman_amd/_variants/lib_treestamps.so ]; then
-  MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_treestamps.so timeout -k 10 120 python3 scripts/enc_profile.py 16 stamps 2>&1 | grep -v amdgpu.ids || exit 1
+if [ -f ab/lib_treestamps.so ]; then
+  MH_LIB=$GRAFT_REPO_ROOT/ab/lib_treestamps.so timeout -k 10 120 python3 scripts/enc_profile.py 16 stamps 2>&1 | grep -v amdgpu.ids || exit 1
 fi
 for v in default ${VARIANTS:-}; do
-  if [ "$v" = default ]; then unset MH_LIB; else export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$v.so; fi
+  if [ "$v" = default ]; then unset MH_LIB; else export MH_LIB=$GRAFT_REPO_ROOT/ab/lib_$v.so; fi
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/encab_$v -o enc -- python3 scripts/enc_profile.py 64 > gpurun_out/encab_$v.log 2>&1 || exit 1
   echo "== $v: $(grep async gpurun_out/encab_$v.log)"
   python3 - "$v" <<'PY' || exit 1

@@ -9,7 +9,7 @@ tail -1 gpurun_out/pytest_enc.log
 : > gpurun_out/enc_ab.txt
 for rep in 1 2; do
 for v in default ${ENC_VARIANTS:-tree_bsearch}; do
-  if [ $v = default ]; then unset MH_LIB; else export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$v.so; fi
+  if [ $v = default ]; then unset MH_LIB; else export MH_LIB=$GRAFT_REPO_ROOT/ab/lib_$v.so; fi
   rm -rf gpurun_out/prof_enc_$v
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_enc_$v -o run -- python3 scripts/enc_profile.py 64 > gpurun_out/enc_$v.log 2>&1 || { tail gpurun_out/enc_$v.log; exit 1; }
   timeout -k 10 120 python3 scripts/enc_profile.py 256 > gpurun_out/enc_plain_$v.log 2>&1 || { tail gpurun_out/enc_plain_$v.log; exit 1; }
@@ -23,7 +23,7 @@ PY
 done
 done
 for v in ${STAMP_VARIANTS:-stamps stamps_bsearch}; do
-  export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$v.so
+  export MH_LIB=$GRAFT_REPO_ROOT/ab/lib_$v.so
   echo "== $v" >> gpurun_out/enc_ab.txt
   timeout -k 10 120 python3 scripts/enc_profile.py 16 stamps >> gpurun_out/enc_ab.txt 2>&1 || { echo "stamps $v failed"; exit 1; }
 done

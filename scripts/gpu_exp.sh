@@ -8,8 +8,8 @@ tail -3 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/pytest_gpu.log | head -20; exit 1; }
 STEPS=${STEPS:-400} bash scripts/gpu_ab.sh || exit 1
 for d in ${DIAGS:-diag}; do
-  [ -f metalhuffman_amd/_variants/lib_$d.so ] || continue
-  export MH_LIB=$GRAFT_REPO_ROOT/metalhuffman_amd/_variants/lib_$d.so
+  [ -f ab/lib_$d.so ] || continue
+  export MH_LIB=$GRAFT_REPO_ROOT/ab/lib_$d.so
   timeout -k 10 300 python scripts/diag_stamps.py --batch 64 ${DIAG_ARGS:-} --tag _$d > gpurun_out/diag64_$d.txt 2>&1 || exit 1
   echo "== $d"; tail -7 gpurun_out/diag64_$d.txt
 done
