@@ -159,14 +159,20 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
     rows(0, bh);
     return MH_OK;
   }
-  // nt - 1 workers; the calling thread decodes the last share itself
+  // nt - 1 workers; the calling thread decodes the last share itself, and every
+  // share no worker could be started for (no exception crosses the C ABI)
   std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (uint32_t t = 0; t + 1 < nt; ++t) {
-    const uint32_t a = (uint32_t)((uint64_t)bh * t / nt), z = (uint32_t)((uint64_t)bh * (t + 1) / nt);
-    th.emplace_back(rows, a, z);
+  uint32_t started = 0;
+  try {
+    th.reserve(nt - 1);
+    for (; started + 1 < nt; ++started) {
+      const uint32_t a = (uint32_t)((uint64_t)bh * started / nt);
+      const uint32_t z = (uint32_t)((uint64_t)bh * (started + 1) / nt);
+      th.emplace_back(rows, a, z);
+    }
+  } catch (...) {
   }
-  rows((uint32_t)((uint64_t)bh * (nt - 1) / nt), bh);
+  rows((uint32_t)((uint64_t)bh * started / nt), bh);
   for (auto &x : th) x.join();
   return MH_OK;
 }

@@ -25,6 +25,7 @@
 
 #include <stdint.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "../../include/metalhuffman.h"
@@ -891,7 +892,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 #define MH_LP_WAVES 4
 #endif
 constexpr int kLpWaves = MH_LP_WAVES;
-constexpr int kLpStageBytes = 3712;   // >= 15 + 32 blocks x 64 x 14 bits / 8 + 24, 16-B multiple
+constexpr int kLpStageBytes = 4144;   // >= 15 + 32 blocks x 64 x 16 bits / 8 + 24, 16-B multiple
+static_assert(kLpStageBytes <= kStageChunks * 64 * 16, "span_issue covers the lane-pair stage");
 constexpr int kLpOutStride = 68;      // bytes per lane row (17 dwords: lanes spread over banks)
 __shared__ __attribute__((aligned(16))) uint16_t s_lp_lut[kLut14Entries];
 __shared__ __attribute__((aligned(16))) uint8_t s_lp_stage[kLpWaves * kLpStageBytes];
@@ -1151,13 +1153,13 @@ __global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const
 }
 
 // Per-device launch parameters (CU count, batch-kernel occupancy per workgroup
-// size), computed once per device ordinal under std::call_once: no mutable state
+// size), computed once per device ordinal under a per-device mutex: no mutable state
 // is shared between devices or written by concurrent callers (the reference keeps
 // its tables in module statics, Shared/HuffmanUtil.cpp:87-102).
 constexpr int kMaxDevices = 64;
 struct DeviceInfo {
-  std::once_flag once;
-  int cus = 0;
+  std::mutex m;
+  std::atomic<int> cus{0};  // nonzero once the entry is complete
   int occ[2][kMaxWavesPerWG + 1] = {};
 };
 DeviceInfo g_devinfo[kMaxDevices];
@@ -1180,24 +1182,27 @@ int stream_device(hipStream_t s) {
   return dev;
 }
 
+// Filled once per device under its mutex; a failed query leaves the entry empty,
+// so the next call tries again (a transient HIP error does not stick).
 const DeviceInfo *device_info(hipStream_t s) {
   const int dev = stream_device(s);
   if (dev < 0 || dev >= kMaxDevices) return nullptr;
   DeviceInfo &d = g_devinfo[dev];
-  std::call_once(d.once, [&] {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
-    int cur = -1;
-    const bool swap = hipGetDevice(&cur) == hipSuccess && cur != dev;
-    if (swap && hipSetDevice(dev) != hipSuccess) return;
-    for (int nw = 1; nw <= kMaxWavesPerWG; ++nw) {
-      d.occ[0][nw] = occupancy_query<false>(nw);
-      d.occ[1][nw] = occupancy_query<true>(nw);
-    }
-    if (swap) (void)hipSetDevice(cur);
-    d.cus = prop.multiProcessorCount;  // last: nonzero marks the entry complete
-  });
-  return d.cus ? &d : nullptr;
+  if (d.cus.load(std::memory_order_acquire)) return &d;
+  std::lock_guard<std::mutex> lock(d.m);
+  if (d.cus.load(std::memory_order_relaxed)) return &d;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess || prop.multiProcessorCount < 1) return nullptr;
+  int cur = -1;
+  const bool swap = hipGetDevice(&cur) == hipSuccess && cur != dev;
+  if (swap && hipSetDevice(dev) != hipSuccess) return nullptr;
+  for (int nw = 1; nw <= kMaxWavesPerWG; ++nw) {
+    d.occ[0][nw] = occupancy_query<false>(nw);
+    d.occ[1][nw] = occupancy_query<true>(nw);
+  }
+  if (swap) (void)hipSetDevice(cur);
+  d.cus.store(prop.multiProcessorCount, std::memory_order_release);  // last: marks the entry complete
+  return &d;
 }
 
 // One kernel launch; any_order (MH_FLAG_ANY_ORDER) clears the dispatch packet's
@@ -1215,7 +1220,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   DecodeArgs a = a0;
   const DeviceInfo *di = device_info(s);
   if (!di) return MH_ERR_HIP;
-  const int cus = di->cus;
+  const int cus = di->cus.load(std::memory_order_relaxed);
   if (lane_pairs && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // experimental lane-pair decode (MH_FLAG_LANE_PAIRS): 32-block tiles
     const uint32_t n_frames = a.total_tiles / a.tiles_per_frame;

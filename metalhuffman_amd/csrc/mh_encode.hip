@@ -40,6 +40,7 @@ constexpr uint32_t kHistParts = MH_HIST_PARTS;  // partial histograms the split 
 constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
 constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is published (fused path)
+constexpr uint32_t kAbort = 19;         // meta[] slot: a packing workgroup gave up waiting (fused path)
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 #ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
 #define MH_FUSED_MAX_TILES 512
@@ -86,7 +87,7 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
-  o += align256((kFlag + 1) * 8);
+  o += align256((kAbort + 1) * 8);
   if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
   o += align256((nb + kCodeTile - 1) / kCodeTile * 256 * 2);
   return o;
@@ -161,7 +162,10 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
                                                         uint32_t vec, uint8_t *sym, uint8_t *block_init,
                                                         uint64_t *hist, uint16_t *tile_hist, uint64_t *meta) {
   const bool tiled = tile_hist != nullptr;
-  if (tiled && blockIdx.x == 0 && threadIdx.x == 0) meta[kFlag] = 0;  // the code kernel runs after this one
+  if (tiled && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
+    meta[kFlag] = 0;
+    meta[kAbort] = 0;
+  }
   MH_SPLIT_STAMP(0)
   __shared__ uint32_t h[256 * kHistCopies];
   for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
@@ -657,17 +661,31 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     meta[kTicket] = 0;
     meta[kTotalBits] = total;
     if (codes_len_out) *codes_len_out = bad ? 0 : len;
-    if (status) *status = bad ? -(int32_t)bad : MH_OK;
+    if (status) {
+      if constexpr (kFused) {
+        // A packing workgroup that timed out (meta[kAbort], then its MH_ERR_HIP status)
+        // must not be overwritten: every access here is sequentially consistent, so
+        // either this load sees the abort, or the packer's status store follows ours.
+        __hip_atomic_store(status, bad ? -(int32_t)bad : MH_OK, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kAbort]), __ATOMIC_SEQ_CST,
+                              __HIP_MEMORY_SCOPE_AGENT))
+          __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *status = bad ? -(int32_t)bad : MH_OK;
+      }
+    }
     published = bad ? 2u : 1u;
   }
   if constexpr (kFused) {
-    // every table store acknowledged (agent scope: past this XCD's L2), then the flag
+    // Publication in the HIP memory model: each thread's table store is released at
+    // agent scope (its own fence), the barrier orders every thread before thread 0,
+    // and the flag is a release store the packers acquire (pack_tile).
     MH_CODE_STAMP(0, 1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     MH_CODE_STAMP(0, 2)
     if (tid == 0)
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), published, __ATOMIC_RELAXED,
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), published, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
   (void)published;
@@ -904,7 +922,10 @@ constexpr uint32_t kCodeThreads = 1024;
 #endif
 constexpr uint32_t kCodeWaves = kCodeThreads / 64;
 constexpr uint32_t kCodeWords = kCodeTile * 64 * 16 / 32 + 2;  // a tile's code words, <= 16-bit codes
-constexpr uint64_t kSpinTicks = 10000000;                       // 100 ms of s_memrealtime (100 MHz)
+#ifndef MH_DIAG_SPIN_TICKS  // diagnostic builds only (tests/test_gpu_encode.py: forced timeout)
+#define MH_DIAG_SPIN_TICKS 10000000
+#endif
+constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;             // 100 ms of s_memrealtime (100 MHz)
 static_assert(kCodeThreads == 8 * kCodeTile, "eight lanes per block");
 
 // Inclusive prefix sum over the wave by DPP (row_shr 1/2/4/8 inside each row of 16
@@ -994,7 +1015,7 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
   if (tid == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t f;
-    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
+    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_ACQUIRE,
                                   __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
         f = 3u;
@@ -1008,10 +1029,16 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
   __syncthreads();
   const uint32_t f = s_flag;
   if (f != 1u) {  // rejected frame (status set by the tree): write nothing
-    if (f == 3u && tid == 0 && status)
-      __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f == 3u && tid == 0) {  // timed out: sticky, whenever the tree's own status lands
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
+  // thread 0's acquire (the flag load) reaches the other threads through the barrier;
+  // each thread's own agent-scope acquire keeps its table loads behind it
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   MH_CODE_STAMP(t + 1, 2)

@@ -43,16 +43,17 @@ def test_roofline_fields_and_arithmetic(bench):
                            read_bytes=2_135_356, kernel_ms=0.00579)
     finally:
         bench.ACHIEVABLE.clear()
-    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_us_avg", "region_us_per_launch",
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_us_avg", "graph_us_per_launch",
               "algorithmic_bytes_per_launch", "frac_of_achievable", "read_frac"):
         assert k in r, k
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
-    assert r["kernel_us_avg"] == pytest.approx(5.79, abs=1e-3)
-    assert r["achieved"] == pytest.approx(5_281_084 / 5.79e-6 / 1e9, rel=1e-3)
+    # the timed region's own events / K, not the 200-launch graph
+    assert r["kernel_us_avg"] == pytest.approx(5.8, abs=1e-3)
+    assert r["achieved"] == pytest.approx(5_281_084 / 5.8e-6 / 1e9, rel=1e-3)
     assert r["frac"] == pytest.approx(r["achieved"] / 8000.0, abs=1e-4)
     assert r["frac_of_achievable"] == pytest.approx(r["achieved"] / 5800.0, abs=1e-4)
-    assert r["region_us_per_launch"] == pytest.approx(5.8, abs=1e-3)
-    assert r["read_frac"] == pytest.approx(2_135_356 / 5.79e-6 / 1e9 / 8000.0, abs=1e-4)
+    assert r["graph_us_per_launch"] == pytest.approx(5.79, abs=1e-3)
+    assert r["read_frac"] == pytest.approx(2_135_356 / 5.8e-6 / 1e9 / 8000.0, abs=1e-4)
     # the committed PMC profile backs the traffic figure of every workload
     for wl in ("frame", "batch", "tile8192", "tile8192_random"):
         t = bench.measured_traffic(wl)

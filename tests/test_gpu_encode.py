@@ -289,3 +289,38 @@ def test_async_encode_workspace_flag(mh, device, bigbridge):
             continue
         r = a.result()
         assert np.array_equal(r.canon, ref.canon) and np.array_equal(r.codes.cpu().numpy(), ref.codes), k
+
+
+def test_fused_encoder_timeout_is_sticky(mh):
+    """A packing workgroup that gives up waiting for the code table (diagnostic build
+    with a zero spin budget, MH_DIAG_SPIN_TICKS=0) must leave MH_ERR_HIP in the status,
+    whenever workgroup 0's own status store lands (mh_encode.hip: meta[kAbort], all
+    four accesses sequentially consistent). Child process: the diagnostic library is
+    loaded through MH_LIB, never beside the default one."""
+    import os
+    import subprocess
+    import sys
+
+    import metalhuffman_amd.build as B
+    lib = B.diag_lib_path("spin0")
+    assert os.path.exists(lib), "build() makes the diagnostic libraries"
+    code = (
+        "import sys, torch; sys.path.insert(0, %r)\n"
+        "import metalhuffman_amd as mh\n"
+        "from metalhuffman_amd import frames as F\n"
+        "from metalhuffman_amd.encoder import Encoder\n"
+        "assert mh.lib().mh_build_stamp().decode().startswith('diag:spin0:')\n"
+        "img = torch.from_numpy(F.bigbridge()).cuda()\n"
+        "enc = Encoder(img.shape[1], img.shape[0], 'cuda')\n"
+        "bad = 0\n"
+        "for _ in range(4):\n"
+        "    try:\n"
+        "        enc.encode(img)\n"
+        "    except mh.MHError as e:\n"
+        "        assert e.status == -7, e\n"
+        "        bad += 1\n"
+        "print('timeouts', bad)\n"
+        "assert bad == 4\n" % B.ROOT)
+    env = dict(os.environ, MH_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
