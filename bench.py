@@ -176,6 +176,23 @@ class Workload:
         for i in range(warmup):
             self.launch(i)
         torch.cuda.synchronize(dev)
+        # Long launches (>= LONG_LAUNCH_US each: the 64-frame batch, the 8192^2 frame) are
+        # timed as plain eager launches: the host enqueues them faster than they run, so
+        # the queue never drains and no gate or graph is needed (a hipGraph replay of 256
+        # such launches cost the host ~2x the GPU time, and under rocprofv3 a long graph
+        # queued behind the gate ran 13-17 % slower per dispatch than the same launches
+        # plainly: profiles/r03_gate_rocprof_artifact.txt). Short launches (one frame,
+        # ~5.6 us) are queued behind the launch gate as before.
+        pa, pb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        npr = min(8, max(1, steps))
+        pa.record()
+        for i in range(npr):
+            self.launch(i)
+        pb.record()
+        torch.cuda.synchronize(dev)
+        self.long_launches = pa.elapsed_time(pb) / npr * 1e3 >= LONG_LAUNCH_US
+        if self.long_launches:
+            use_graph = gate = False
         graph = None
         if use_graph:
             try:
@@ -271,13 +288,7 @@ class Workload:
                 w = float(t.item())
             return w, (r0.elapsed_time(r1) if events else None)
 
-        # The gate only for short regions (<= 64 launches): there the host's enqueue of
-        # the K launches is a visible share of the clock. Long regions (the 256/512-launch
-        # batch and 8192^2 extras) replay their graph plainly: under rocprofv3 a graph
-        # queued behind the gate ran 13-17 % slower per dispatch than the same graph
-        # replayed plainly (profiles/r03_gate_rocprof_artifact.txt), so a gated long
-        # region could not be checked against the profiler.
-        if gate and GATE.ok() and steps <= 64:
+        if gate and GATE.ok():
             timed(True)  # the gate's own first launch off the clock
             # The clocked region holds only the K launches: its two HIP event records
             # (markers in the queue) cost ~7 us per region at 20 steps (510 vs 482 x10^3
@@ -294,7 +305,9 @@ class Workload:
         else:
             wall, region_ms = timed(False)
             self.ungated_wall = None
-            self.timed_launch = "hipGraph" if graph is not None else "eager"
+            self.timed_launch = ("hipGraph" if graph is not None else
+                                 "eager (long launches: the host enqueues ahead of the GPU)"
+                                 if self.long_launches else "eager")
         # Per-launch kernel duration: the same K-launch graph replayed back to back
         # (>= 200 launches) between one event pair on the launch stream, so the fixed
         # cost of opening a region (gate release, first dispatch: ~13 us measured)
@@ -320,7 +333,7 @@ class Workload:
             self.kernel_ms = ka.elapsed_time(kb) / nk
             del kg
         else:
-            self.kernel_ms = self.region_kernel_ms
+            self.kernel_ms = None
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
         for i in range(steps):
@@ -333,6 +346,7 @@ class Workload:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+LONG_LAUNCH_US = 20.0  # Workload.run: launches at least this long are timed as plain eager launches
 
 
 def measured_traffic(workload: str):

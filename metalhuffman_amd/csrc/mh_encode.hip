@@ -677,11 +677,11 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     published = bad ? 2u : 1u;
   }
   if constexpr (kFused) {
-    // Publication in the HIP memory model: each thread's table store is released at
-    // agent scope (its own fence), the barrier orders every thread before thread 0,
-    // and the flag is a release store the packers acquire (pack_tile).
+    // Publication in the HIP memory model: every thread's table store (an agent-scope
+    // atomic) happens-before thread 0's flag store through the workgroup barrier, and
+    // the flag store is an agent-scope release that the packers' acquire pairs with
+    // (pack_tile): release/acquire, no reliance on vmcnt ordering.
     MH_CODE_STAMP(0, 1)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     MH_CODE_STAMP(0, 2)
     if (tid == 0)
@@ -1015,7 +1015,9 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
   if (tid == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t f;
-    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_ACQUIRE,
+    // relaxed polls (an acquire per poll would invalidate caches on every iteration),
+    // then one agent-scope acquire fence once the flag is seen
+    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
         f = 3u;
@@ -1023,6 +1025,7 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the tree's release store
     s_flag = f;
   }
   MH_CODE_STAMP(t + 1, 1)
@@ -1036,9 +1039,8 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
     }
     return;
   }
-  // thread 0's acquire (the flag load) reaches the other threads through the barrier;
-  // each thread's own agent-scope acquire keeps its table loads behind it
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // thread 0's acquire reaches the table readers through the workgroup barrier above
+  // (happens-before is transitive), and the table loads are agent-scope atomics
   if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   MH_CODE_STAMP(t + 1, 2)

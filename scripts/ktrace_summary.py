@@ -4,7 +4,7 @@ Grouped by kernel and launch shape; compare with the bench line's
 roofline.kernel_us_avg of the same command (scripts/gpu_check.sh profiles one
 workload per command). Counts include warm-up, the untimed first graph replay,
 the timed graph replay and the eager per-launch pass (bench.Workload.run), all
-the same launch. `timed_avg` is the mean over the timed replay alone, K = --steps of
+the same launch. `timed_avg` (and timed_span/K, first start to last end / K) is over the timed region alone, K = --steps of
 the profiled command (default 200): the K decode launches that follow the last
 launch-gate kernel (bench.py's gated region, scripts/micro/launch_gate.hip), or, in a
 trace without the gate, launches [n - 2K, n - K) in start order.
@@ -30,18 +30,40 @@ for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
         key = (r["Kernel_Name"].split("mh_decode")[1].split("_kernel")[0] or "batch", int(r["Grid_Size_X"]),
                int(r["Workgroup_Size_X"]), int(r["LDS_Block_Size"]), int(r["VGPR_Count"]))
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        groups[key].append((s, (e - s) / 1e3))
+        groups[key].append((s, e))
+
+
+def runs_of(d, gap_ns=20000):
+    """Back-to-back runs (next start within gap_ns of the previous end)."""
+    out, cur = [], []
+    for s, e in d:
+        if cur and s - cur[-1][1] > gap_ns:
+            out.append(cur)
+            cur = []
+        cur.append((s, e))
+    if cur:
+        out.append(cur)
+    return out
+
+
 print(f"{'kernel':>8} {'grid_threads':>12} {'wg':>5} {'lds':>6} {'vgpr':>5} {'n':>5} {'avg_us':>9} "
-      f"{'median_us':>9} {'min_us':>8} {'timed_avg':>9}")
+      f"{'median_us':>9} {'min_us':>8} {'timed_avg':>9} {'timed_span/K':>12}")
 for (k, g, w, lds, v), d in sorted(groups.items(), key=lambda kv: -len(kv[1])):
     d.sort()
-    dur = [x for _, x in d]
+    dur = [(e - s) / 1e3 for s, e in d]
     n = len(dur)
+    # the timed region: the K launches after the last launch gate (gated regions), or
+    # else the run of K launches followed by exactly two more runs (bench.Workload.run:
+    # timed replay, then the >=200-launch graph, then the eager per-launch pass)
+    timed = []
     if gates:
-        after = [x for t, x in d if t > max(gates)]
-        timed = after[:steps] if len(after) >= steps else []
+        timed = [x for x in d if x[0] > max(gates)][:steps]
+        timed = timed if len(timed) == steps else []
     else:
-        timed = dur[n - 2 * steps: n - steps] if n >= 2 * steps else []
-    ta = f"{statistics.mean(timed):9.3f}" if timed else f"{'-':>9}"
+        rs = [r for r in runs_of(d) if len(r) >= steps]
+        if len(rs) >= 3 and len(rs[-3]) == steps:
+            timed = rs[-3]
+    ta = f"{statistics.mean((e - s) / 1e3 for s, e in timed):9.3f}" if timed else f"{'-':>9}"
+    sp = f"{(timed[-1][1] - timed[0][0]) / 1e3 / len(timed):12.3f}" if timed else f"{'-':>12}"
     print(f"{k:>8} {g:12d} {w:5d} {lds:6d} {v:5d} {n:5d} {statistics.mean(dur):9.3f} "
-          f"{statistics.median(dur):9.3f} {min(dur):8.3f} {ta}")
+          f"{statistics.median(dur):9.3f} {min(dur):8.3f} {ta} {sp}")
