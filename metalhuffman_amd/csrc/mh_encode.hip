@@ -41,6 +41,8 @@ constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's com
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
 constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is published (fused path)
 constexpr uint32_t kAbort = 19;         // meta[] slot: a packing workgroup gave up waiting (fused path)
+constexpr uint32_t kHistDone = 20;      // meta[] slot: tiles whose counts are in hist (one-launch path)
+constexpr uint32_t kDone = 21;          // meta[] slot: packing workgroups finished (one-launch path)
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 #ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
 #define MH_FUSED_MAX_TILES 512
@@ -69,6 +71,8 @@ struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint32_t *table;    // 256 x (code_lj16 << 16 | len)
   uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits], [kFlag]]
   uint16_t *tile_hist;  // fused path: ceil(nb / kCodeTile) x 256 symbol counts
+  uint64_t *tstate;     // one-launch path: per code tile, look-back state (flag << 62 | bits)
+  uint32_t *claim;      // one-launch path: per code tile, who added its counts (1 itself, 2 the tree)
 };
 
 constexpr uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -86,10 +90,16 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   o += align256(kHistParts * 256 * 8);
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
+  // meta, tstate and claim are contiguous: the one-launch path's state, zeroed together
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
-  o += align256((kAbort + 1) * 8);
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  o += align256((kDone + 1) * 8);
+  if (w) w->tstate = reinterpret_cast<uint64_t *>(base + o);
+  o += align256(ncode * 8);
+  if (w) w->claim = reinterpret_cast<uint32_t *>(base + o);
+  o += align256(ncode * 4);
   if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
-  o += align256((nb + kCodeTile - 1) / kCodeTile * 256 * 2);
+  o += align256(ncode * 256 * 2);
   return o;
 }
 
@@ -1149,19 +1159,313 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kern
   pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, status);
 }
 
+// ---- the one-launch path: enc_one_kernel ------------------------------------------
+// One launch for frames of <= MH_FUSED_MAX_TILES code tiles, each pixel read once.
+// Workgroup t + 1 loads tile t's pixels (kept in registers), derives the symbols, counts
+// them in LDS and adds the counts into the partial histograms; workgroup 0 waits until
+// every tile's counts are in (a published-tiles counter; a tile whose workgroup has not
+// started after a bounded wait is claimed and counted by workgroup 0 itself, so the
+// launch cannot deadlock however few workgroups are resident), builds the tree
+// (tree_body<true>) and publishes the code table. Each packing workgroup then takes its
+// own tile's bit count (its counts x code lengths) and finds its first bit by a
+// decoupled look-back over the tiles before it (each tile publishes its aggregate, then
+// its inclusive prefix), instead of re-reading every earlier tile's histogram. The last
+// workgroup to finish re-zeroes the launch state for the next frame.
+constexpr uint64_t kAggFlag = 1ull << 62, kInclFlag = 2ull << 62, kValMask = (1ull << 62) - 1ull;
+#ifndef MH_ONE_CLAIM_TICKS  // workgroup 0's wait before it counts missing tiles itself (s_memrealtime, 100 MHz)
+#define MH_ONE_CLAIM_TICKS 2000  // 20 us
+#endif
+
+// Counts of tile t's symbols into h (256 x kHistCopies words of LDS, zeroed) by all
+// kCodeThreads threads; returns this lane's symbols (q) and its row pixels' block.
+__device__ __forceinline__ uint64_t tile_symbols(const Pixels px, uint64_t nb, uint32_t t, uint32_t *h,
+                                                 uint32_t *first) {
+  const uint32_t tid = threadIdx.x, part = tid & 7u;
+  const uint64_t b = (uint64_t)t * kCodeTile + (tid >> 3);
+  const uint64_t g = block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b, part);
+  const uint64_t q = row_symbols(g, part, px.delta, px.init_byte, first);
+  if (b < nb) {
+    const uint32_t copy = tid % kHistCopies;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(q >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+  }
+  return q;
+}
+
+// Workgroup 0, before the tree: every tile's counts in hist.
+__device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *hist,
+                                                uint64_t *meta, uint32_t *claim, uint32_t *h) {
+  __shared__ uint32_t s_next, s_mine;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) < ntiles &&
+           __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)MH_ONE_CLAIM_TICKS)
+      __builtin_amdgcn_s_sleep(2);
+    s_mine = 0;
+    s_next = 0;
+  }
+  __syncthreads();
+  // tiles nobody has claimed yet: count them here (rare; the packer that starts later
+  // finds its claim taken and leaves the histogram alone)
+  for (;;) {
+    if (tid == 0) {
+      uint32_t t = s_next;
+      for (; t < ntiles; ++t) {
+        uint32_t z = 0;
+        if (__hip_atomic_load(&claim[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+            __hip_atomic_compare_exchange_strong(&claim[t], &z, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;
+      }
+      s_next = t;
+    }
+    __syncthreads();
+    const uint32_t t = s_next;
+    if (t >= ntiles) break;
+    for (uint32_t i = tid; i < 256 * kHistCopies; i += kCodeThreads) h[i] = 0;
+    __syncthreads();
+    uint32_t first_unused;
+    tile_symbols(px, nb, t, h, &first_unused);
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t c = 0;
+      for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
+      if (c) atomicAdd((unsigned long long *)&hist[(t % kHistParts) * 256 + tid], (unsigned long long)c);
+    }
+    if (tid == 0) {
+      ++s_mine;
+      ++s_next;
+    }
+    __syncthreads();
+  }
+  // then the tiles whose own workgroups claimed them: all of their adds published
+  if (tid == 0) {
+    while (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) + s_mine < ntiles)
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with each packer's release increment
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint64_t *hist, const uint32_t *table,
+                                              uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint64_t nb,
+                                              uint32_t ntiles, uint32_t *offsets, uint32_t *words, int32_t *status,
+                                              uint32_t *h, uint8_t *block_init) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t lw[kCodeWords];
+  __shared__ uint32_t s_cnt[256];
+  __shared__ uint32_t s_dot[4], s_scan[kCodeWaves];
+  __shared__ uint32_t s_flag, s_E;
+  const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
+  const bool on = b < nb;
+  for (uint32_t i = tid; i < 256 * kHistCopies; i += kCodeThreads) h[i] = 0;
+  // (lanes 0-7, t > 0) the previous block's rows: the head bits of this tile's first word
+  const uint64_t gp = (t > 0 && tid < 8) ? block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
+  __syncthreads();
+  uint32_t first, first_unused;
+  const uint64_t q = tile_symbols(px, nb, t, h, &first);
+  if (block_init && part == 0 && on) block_init[b] = (uint8_t)first;  // AAPLRenderer.m:449-473
+  const uint64_t qp = row_symbols(gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // lanes 0-7 of wave 0
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
+    s_cnt[tid] = c;
+  }
+  if (tid == 0) {  // this tile's counts go into hist unless workgroup 0 took the tile over
+    uint32_t z = 0;
+    s_flag = __hip_atomic_compare_exchange_strong(&claim[t], &z, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool mine = s_flag != 0;
+  if (mine && tid < 256 && s_cnt[tid])
+    atomicAdd((unsigned long long *)&hist[(t % kHistParts) * 256 + tid], (unsigned long long)s_cnt[tid]);
+  __syncthreads();  // every add of this workgroup happens-before thread 0's release below
+  if (tid == 0) {
+    if (mine)
+      __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 1u, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    // the code table (workgroup 0): relaxed polls, then one acquire fence
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t f;
+    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
+        f = 3u;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_flag = f;
+  }
+  __syncthreads();
+  const uint32_t f = s_flag;
+  if (f == 1u) {
+    if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    // this tile's bit count: its counts x code lengths
+    if (wave < 4) {
+      const uint32_t x = wave_scan_dpp(s_cnt[tid] * (tab[tid] & 0xFFu));
+      if (lane == 63) s_dot[wave] = x;
+    }
+    // this lane's codes, as two chunks of four (<= 64 bits each)
+    uint64_t ch[2] = {0, 0};
+    uint32_t cl[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t e = tab[(uint32_t)(q >> (8 * j)) & 0xFFu];
+      const uint32_t len = e & 0xFFu;
+      ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
+      cl[j >> 2] += len;
+    }
+    const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
+    const uint32_t incl = wave_scan_dpp(nbits);
+    if (lane == 63) s_scan[wave] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      // decoupled look-back: publish the aggregate, sum the tiles before this one
+      // back to the first published inclusive prefix, publish the inclusive prefix
+      const uint64_t agg = (uint64_t)s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
+      uint64_t E = 0;
+      bool ok = true;
+      if (t > 0) {
+        __hip_atomic_store(&tstate[t], kAggFlag | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t u = t - 1; ok; --u) {
+          uint64_t v;
+          while (((v = __hip_atomic_load(&tstate[u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0u) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // a tile before gave up: so do we
+              ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          E += v & kValMask;
+          if ((v >> 62) == 2u) break;
+        }
+      }
+      if (ok) __hip_atomic_store(&tstate[t], kInclFlag | (E + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      s_E = (uint32_t)E;
+      s_flag = ok ? 1u : 3u;
+    }
+    if (wave == 0) {
+      const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
+      if (lane < kCodeWaves) s_scan[lane] = v;
+    }
+    __syncthreads();
+    if (s_flag != 1u) {
+      if (tid == 0) {
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      goto finish;
+    }
+    {
+    const uint32_t E = s_E;
+    const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
+    const uint32_t T = s_scan[kCodeWaves - 1];
+    if (on && part == 0) offsets[b] = E + pre;
+    const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
+    const uint32_t nwords = ((end + 31u) >> 5) - w0;
+    for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
+    // the previous block's last r bits, the head of this tile's first word (lanes 0-7)
+    uint32_t head = 0;
+    if (r && wave == 0) {
+      uint32_t lenp = 0;
+      uint64_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
+        const uint32_t len = e & 0xFFu;
+        acc = (acc << len) | ((e >> 16) >> (16 - len));
+        lenp += len;
+      }
+      if (lane >= 8) lenp = 0;
+      const uint32_t incp = wave_scan_dpp(lenp);
+      const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
+      if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
+      for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
+    }
+    __syncthreads();
+    if (on) {
+      or_bits(lw, r + pre, ch[0], cl[0]);
+      or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
+    }
+    if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
+    __syncthreads();
+    const bool last = t + 1 == ntiles;
+    const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
+    for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
+    if (last) {
+      const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
+      for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
+    }
+    }
+  } else if (f == 3u && tid == 0) {  // timed out: sticky, whenever the tree's own status lands
+    __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+    if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the last packing workgroup to finish re-zeroes the launch state for the next frame
+  // (every other workgroup's look-back is over by then: each waits only on earlier tiles,
+  // and all of them have finished)
+finish:
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t done = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kDone]), 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_flag = done + 1u == ntiles ? 1u : 0u;
+  }
+  __syncthreads();
+  if (s_flag) {
+    for (uint32_t i = tid; i < ntiles; i += kCodeThreads) {
+      __hip_atomic_store(&tstate[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&claim[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) {
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kDone]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kernel(
+    uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta, uint64_t *codes_len_out, uint64_t codes_cap,
+    int32_t *status, const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *tstate, uint32_t *claim,
+    uint32_t *offsets, uint32_t *words, uint8_t *block_init) {
+  __shared__ uint32_t s_h[256 * kHistCopies];  // one tile's symbol counts, kHistCopies copies
+  if (blockIdx.x == 0) {
+    wait_histograms(px, nb, ntiles, hist, meta, claim, s_h);
+    tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
+    return;
+  }
+  pack_tile_one(blockIdx.x - 1, px, hist, table, meta, tstate, claim, nb, ntiles, offsets, words, status, s_h,
+                block_init);
+}
+
 }  // namespace
 
 extern "C" {
 
 // MH_ENCODE_KERNELS=4 selects the four-kernel path (split, tree, scan, pack) for
-// every frame size (A/B and tests); frames of more than MH_FUSED_MAX_TILES tiles
-// always take it (a packing workgroup sums the histograms of every tile before it).
-static bool four_kernel_path() {
-  static const bool four = [] {
+// every frame size, =2 the two-launch path (split, then tree + packing with every
+// earlier tile's histogram summed per tile) -- A/B and tests. By default frames of
+// <= MH_FUSED_MAX_TILES code tiles take the one-launch path (enc_one_kernel), larger
+// ones the four-kernel path (workgroup 0 would count many non-resident tiles alone).
+static int encode_kernels() {
+  static const int k = [] {
     const char *v = std::getenv("MH_ENCODE_KERNELS");
-    return v && std::strcmp(v, "4") == 0;
+    return v ? std::atoi(v) : 1;
   }();
-  return four;
+  return k;
 }
 
 // mh_encode_frame_device_async's workspace; mh_encode_frame_device needs kResultBytes
@@ -1215,13 +1519,25 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const uint64_t ntiles = (nb + kScanTile - 1) / kScanTile;
   if (g256 == 0 || ntiles > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
 
-  // the tree kernel zeroes the histogram after reading it, for the next call
-  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) && hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess)
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  // the tree zeroes the histogram after reading it and the one-launch path's last
+  // workgroup its state, for the next call
+  const size_t state_bytes = align256((kDone + 1) * 8) + align256(ncode * 8) + align256(ncode * 4);
+  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) &&
+      (hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess ||
+       hipMemsetAsync(w.meta, 0, state_bytes, s) != hipSuccess))
     return MH_ERR_HIP;
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
-  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
-  if (ncode <= MH_FUSED_MAX_TILES && !four_kernel_path()) {
+  const int path = encode_kernels();
+  if (ncode <= MH_FUSED_MAX_TILES && path == 1) {
+    const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
+    hipLaunchKernelGGL(enc_one_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist, d_canon_header,
+                       w.table, w.meta, d_codes_len, codes_cap, d_status, px, nb, (uint32_t)ncode, w.tstate, w.claim,
+                       d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), d_block_init);
+    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
+  }
+  if (ncode <= MH_FUSED_MAX_TILES && path == 2) {
     // two launches: the tiled split, then tree + offsets + packing in one kernel
     hipLaunchKernelGGL(enc_split_kernel, dim3((uint32_t)ncode), dim3(256), 0, s, d_gray, width, height, bw, nb,
                        flags, vec, nullptr, d_block_init, w.hist, w.tile_hist, w.meta);

@@ -8,7 +8,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -1 gpurun_out/pytest_gpu.log; grep -c PASSED gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
 echo "smoke ok"
-timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 : > gpurun_out/ktrace_summary.txt
 # same steps / warm-up as the bench line each number is compared with (the frame

@@ -57,8 +57,8 @@ def test_encode_8192_tile(mh, device, bigbridge):
 
 @pytest.mark.parametrize("hw", [(2048, 2048), (2056, 2048), (8, 65528), (2048, 1536)])
 def test_async_encode_fused_path_boundary(mh, device, bigbridge, hw):
-    """Frames of up to 512 tiles of 128 blocks take the two-launch path (tiled split +
-    code kernel), larger ones the four-kernel path. (h, w) = (2048, 2048) is exactly
+    """Frames of up to 512 tiles of 128 blocks take the one-launch path (enc_one_kernel),
+    larger ones the four-kernel path. (h, w) = (2048, 2048) is exactly
     512 tiles, (2056, 2048) 514, (8, 65528) one block row of 8191 blocks (64 tiles,
     the last partial), (2048, 1536) BigBridge's shape transposed. Both sides
     byte-identical to the host codec."""
@@ -324,3 +324,36 @@ def test_fused_encoder_timeout_is_sticky(mh):
     env = dict(os.environ, MH_LIB=lib)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("path", ["2", "4"])
+def test_encoder_alternative_paths(mh, path):
+    """The one-launch path is the default for frames of <= 512 code tiles; the two-launch
+    (MH_ENCODE_KERNELS=2: tiled split + code kernel) and four-kernel (=4) paths stay
+    selectable and byte-identical to the host codec. The knob is read once per process,
+    so each path runs in a child process."""
+    import os
+    import subprocess
+    import sys
+
+    import metalhuffman_amd.build as B
+    code = (
+        "import sys, numpy as np, torch; sys.path.insert(0, %r)\n"
+        "import metalhuffman_amd as mh\n"
+        "from metalhuffman_amd import frames as F\n"
+        "from metalhuffman_amd.encoder import Encoder\n"
+        "bb = F.bigbridge()\n"
+        "for img, init in ((bb, False), (np.ascontiguousarray(bb[:777, :1001]), True), (F.uniform_random(256, 320, 77), False)):\n"
+        "    ref = mh.encode_frame(img, init_zero_delta=init)\n"
+        "    enc = Encoder(img.shape[1], img.shape[0], 'cuda')\n"
+        "    for _ in range(2):\n"
+        "        a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).cuda(), 0, init)\n"
+        "        r = a.result()\n"
+        "        assert np.array_equal(r.canon, ref.canon)\n"
+        "        assert np.array_equal(r.codes.cpu().numpy(), ref.codes)\n"
+        "        assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)\n"
+        "        if init: assert np.array_equal(a.block_init.cpu().numpy(), ref.block_init)\n"
+        "print('ok')\n" % B.ROOT)
+    env = dict(os.environ, MH_ENCODE_KERNELS=path)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
