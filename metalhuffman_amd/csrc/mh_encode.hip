@@ -1250,6 +1250,31 @@ __device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, ui
   __syncthreads();
 }
 
+// The last workgroup of the launch to get here (the ntiles packers and workgroup 0, once
+// its table is out) re-zeroes the launch state for the next frame: by then no look-back,
+// claim or histogram wait can still read it. `nthreads` threads of the workgroup call it.
+__device__ __forceinline__ void finish_launch(uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint32_t ntiles,
+                                              uint32_t nthreads) {
+  __shared__ uint32_t s_last;
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t done = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kDone]), 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_last = done == ntiles ? 1u : 0u;  // ntiles + 1 participants
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (uint32_t i = tid; i < ntiles; i += nthreads) {
+    __hip_atomic_store(&tstate[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&claim[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) {
+    for (uint32_t k : {kHistDone, kFlag, kAbort, kDone})
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[k]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint64_t *hist, const uint32_t *table,
                                               uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint64_t nb,
                                               uint32_t ntiles, uint32_t *offsets, uint32_t *words, int32_t *status,
@@ -1412,29 +1437,8 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
     __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // the last packing workgroup to finish re-zeroes the launch state for the next frame
-  // (every other workgroup's look-back is over by then: each waits only on earlier tiles,
-  // and all of them have finished)
 finish:
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t done = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kDone]), 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    s_flag = done + 1u == ntiles ? 1u : 0u;
-  }
-  __syncthreads();
-  if (s_flag) {
-    for (uint32_t i = tid; i < ntiles; i += kCodeThreads) {
-      __hip_atomic_store(&tstate[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&claim[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid == 0) {
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kDone]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  finish_launch(meta, tstate, claim, ntiles, kCodeThreads);
 }
 
 __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kernel(
@@ -1445,6 +1449,8 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kerne
   if (blockIdx.x == 0) {
     wait_histograms(px, nb, ntiles, hist, meta, claim, s_h);
     tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
+    // tree_body ends with the 256 symbol threads (the other waves have exited)
+    finish_launch(meta, tstate, claim, ntiles, 256);
     return;
   }
   pack_tile_one(blockIdx.x - 1, px, hist, table, meta, tstate, claim, nb, ntiles, offsets, words, status, s_h,

@@ -25,6 +25,8 @@ def _dev(device) -> torch.device:
     d = torch.device(device)
     if d.type != "cuda":
         raise RuntimeError("the MI355X decoder needs a HIP device (torch 'cuda' on ROCm)")
+    if d.index is None:  # 'cuda' -> the current device, so device checks compare equal
+        d = torch.device("cuda", torch.cuda.current_device())
     return d
 
 

@@ -345,9 +345,9 @@ def test_encoder_alternative_paths(mh, path):
         "bb = F.bigbridge()\n"
         "for img, init in ((bb, False), (np.ascontiguousarray(bb[:777, :1001]), True), (F.uniform_random(256, 320, 77), False)):\n"
         "    ref = mh.encode_frame(img, init_zero_delta=init)\n"
-        "    enc = Encoder(img.shape[1], img.shape[0], 'cuda')\n"
+        "    enc = Encoder(img.shape[1], img.shape[0], 'cuda:0')\n"
         "    for _ in range(2):\n"
-        "        a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).cuda(), 0, init)\n"
+        "        a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).to('cuda:0'), 0, init)\n"
         "        r = a.result()\n"
         "        assert np.array_equal(r.canon, ref.canon)\n"
         "        assert np.array_equal(r.codes.cpu().numpy(), ref.codes)\n"
