@@ -176,21 +176,15 @@ class Workload:
         for i in range(warmup):
             self.launch(i)
         torch.cuda.synchronize(dev)
-        # Long launches (>= LONG_LAUNCH_US each: the 64-frame batch, the 8192^2 frame) are
-        # timed as plain eager launches: the host enqueues them faster than they run, so
-        # the queue never drains and no gate or graph is needed (a hipGraph replay of 256
-        # such launches cost the host ~2x the GPU time, and under rocprofv3 a long graph
-        # queued behind the gate ran 13-17 % slower per dispatch than the same launches
-        # plainly: profiles/r03_gate_rocprof_artifact.txt). Short launches (one frame,
-        # ~5.6 us) are queued behind the launch gate as before.
-        pa, pb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        npr = min(8, max(1, steps))
-        pa.record()
-        for i in range(npr):
-            self.launch(i)
-        pb.record()
-        torch.cuda.synchronize(dev)
-        self.long_launches = pa.elapsed_time(pb) / npr * 1e3 >= LONG_LAUNCH_US
+        # Long launches (>= LONG_LAUNCH_PIXELS decoded per launch: the 64-frame batch, the
+        # 8192^2 frame; 20-70 us each) are timed as plain eager launches: the host enqueues
+        # them faster than they run, so the queue never drains and no gate or graph is
+        # needed (a hipGraph replay of 256 such launches cost the host ~2x the GPU time,
+        # and under rocprofv3 a long graph queued behind the gate ran 13-17 % slower per
+        # dispatch than the same launches plainly: profiles/r03_gate_rocprof_artifact.txt).
+        # Short launches (one 2048x1536 frame, ~5.5 us) are queued behind the launch gate.
+        # Decided by size, not by a timing probe: under a profiler the probe itself slows.
+        self.long_launches = self.pixels >= LONG_LAUNCH_PIXELS
         if self.long_launches:
             use_graph = gate = False
         graph = None
@@ -241,7 +235,7 @@ class Workload:
         # start costs most; over 256 launches of the 64-frame batch the eager dispatches
         # ran 68.2 vs 63.6 us each (graph), so long regions keep the replay
         eager_gated = GATED_EAGER and steps <= 64
-        def timed(gated, events=True):
+        def timed(gated, events=True, mark=False):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
             opening synchronize, and the clock starts when the host opens it -- every
@@ -249,6 +243,9 @@ class Workload:
             r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if dist.is_initialized():
                 dist.barrier()
+            st = torch.cuda.current_stream(dev).cuda_stream
+            if mark and GATE.ok():
+                GATE.marker(st, 1)  # before the gate / the first launch: off the clock
             torch.cuda.synchronize(dev)
             if gated:
                 GATE.arm(torch.cuda.current_stream(dev).cuda_stream)
@@ -278,6 +275,8 @@ class Workload:
                     for i in range(steps):
                         self.launch(i)
                 r1.record()
+            if mark and GATE.ok():
+                GATE.marker(st, 2)  # after the last launch (one empty kernel inside a plain region's wall)
             torch.cuda.synchronize(dev)
             w = time.perf_counter() - t0
             if dist.is_initialized():
@@ -296,14 +295,14 @@ class Workload:
             # region is a second, identical one. MH_BENCH_REGION_EVENTS=1 keeps them inside.
             if os.environ.get("MH_BENCH_REGION_EVENTS", "0") == "0":
                 wall, _ = timed(True, events=False)
-                _, region_ms = timed(True)
+                _, region_ms = timed(True, mark=True)
             else:
-                wall, region_ms = timed(True)
+                wall, region_ms = timed(True, mark=True)
             self.ungated_wall, _ = timed(False)
             self.timed_launch = (("eager behind the launch gate" + (", launches 2..K with MH_FLAG_ANY_ORDER" if ANY_ORDER else ""))
                                  if eager_gated else "hipGraph behind the launch gate")
         else:
-            wall, region_ms = timed(False)
+            wall, region_ms = timed(False, mark=True)
             self.ungated_wall = None
             self.timed_launch = ("hipGraph" if graph is not None else
                                  "eager (long launches: the host enqueues ahead of the GPU)"
@@ -346,7 +345,7 @@ class Workload:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
-LONG_LAUNCH_US = 20.0  # Workload.run: launches at least this long are timed as plain eager launches
+LONG_LAUNCH_PIXELS = 16 << 20  # Workload.run: launches decoding this many pixels are timed as plain eager launches
 
 
 def measured_traffic(workload: str):
@@ -385,6 +384,7 @@ class _Gate:
             lib.gate_create.argtypes = [ctypes.POINTER(ctypes.c_void_p)] * 2
             lib.gate_arm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
             lib.gate_open.argtypes = [ctypes.c_void_p]
+            lib.trace_marker.argtypes = [ctypes.c_void_p, ctypes.c_uint]
             h, d = ctypes.c_void_p(), ctypes.c_void_p()
             if lib.gate_create(ctypes.byref(h), ctypes.byref(d)) != 0:
                 return False
@@ -392,30 +392,14 @@ class _Gate:
         return True
 
     def arm(self, stream: int) -> None:
-        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "busy":  # A/B: CUs kept busy while closed
-            import ctypes
-            if not hasattr(self, "_dflag"):
-                self._dflag = torch.zeros(64, dtype=torch.int32, device="cuda")
-                self.lib.gate_arm_busy.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
-            nwg = int(os.environ.get("MH_BENCH_GATE_WGS", "1024"))
-            if self.lib.gate_arm_busy(self.h, self.d, self._dflag.data_ptr(), stream, 200_000, nwg,
-                                      self._dflag.data_ptr() + 128) != 0:
-                raise RuntimeError("launch gate: busy kernel launch failed")
-            return
-        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "tight":  # A/B: relaxed polls, no sleep
-            import ctypes
-            self.lib.gate_arm_tight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
-            if self.lib.gate_arm_tight(self.h, self.d, stream, 200_000) != 0:
-                raise RuntimeError("launch gate: kernel launch failed")
-            return
-        if os.environ.get("MH_BENCH_GATE_KIND", "kernel") == "wait":  # A/B: stream wait on the flag
-            import ctypes
-            self.lib.gate_arm_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-            if self.lib.gate_arm_wait(self.h, self.d, stream) != 0:
-                raise RuntimeError("launch gate: stream wait failed")
-            return
         if self.lib.gate_arm(self.h, self.d, stream, 200_000) != 0:  # opens by itself after 200 ms
             raise RuntimeError("launch gate: kernel launch failed")
+
+    def marker(self, stream: int, tag: int) -> None:
+        """An empty kernel on `stream`: brackets the events-timed region in a rocprofv3
+        trace (scripts/ktrace_summary.py)."""
+        if self.lib is not None and self.lib.trace_marker(stream, tag) != 0:
+            raise RuntimeError("trace marker: kernel launch failed")
 
     def open(self) -> None:
         self.lib.gate_open(self.h)

@@ -43,6 +43,7 @@ constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is publis
 constexpr uint32_t kAbort = 19;         // meta[] slot: a packing workgroup gave up waiting (fused path)
 constexpr uint32_t kHistDone = 20;      // meta[] slot: tiles whose counts are in hist (one-launch path)
 constexpr uint32_t kDone = 21;          // meta[] slot: packing workgroups finished (one-launch path)
+constexpr uint32_t kGen = 22;           // meta[] slot: the one-launch path's call generation (1..65535)
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 #ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
 #define MH_FUSED_MAX_TILES 512
@@ -93,13 +94,15 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   // meta, tstate and claim are contiguous: the one-launch path's state, zeroed together
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
   const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
-  o += align256((kDone + 1) * 8);
+  o += align256((kGen + 1) * 8);
   if (w) w->tstate = reinterpret_cast<uint64_t *>(base + o);
   o += align256(ncode * 8);
   if (w) w->claim = reinterpret_cast<uint32_t *>(base + o);
   o += align256(ncode * 4);
+  // two-launch path: u16 counts per tile; one-launch path: u64 words of two
+  // generation-tagged u32 counts per tile (gen << 16 | count), so no zeroing per call
   if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
-  o += align256(ncode * 256 * 2);
+  o += align256(ncode * 256 * 4);
   return o;
 }
 
@@ -1162,16 +1165,16 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kern
 // ---- the one-launch path: enc_one_kernel ------------------------------------------
 // One launch for frames of <= MH_FUSED_MAX_TILES code tiles, each pixel read once.
 // Workgroup t + 1 loads tile t's pixels (kept in registers), derives the symbols, counts
-// them in LDS and adds the counts into the partial histograms; workgroup 0 waits until
-// every tile's counts are in (a published-tiles counter; a tile whose workgroup has not
-// started after a bounded wait is claimed and counted by workgroup 0 itself, so the
-// launch cannot deadlock however few workgroups are resident), builds the tree
-// (tree_body<true>) and publishes the code table. Each packing workgroup then takes its
-// own tile's bit count (its counts x code lengths) and finds its first bit by a
-// decoupled look-back over the tiles before it (each tile publishes its aggregate, then
-// its inclusive prefix), instead of re-reading every earlier tile's histogram. The last
-// workgroup to finish re-zeroes the launch state for the next frame.
-constexpr uint64_t kAggFlag = 1ull << 62, kInclFlag = 2ull << 62, kValMask = (1ull << 62) - 1ull;
+// them in LDS and publishes the counts as generation-tagged words; workgroup 0 sums every
+// tile's words (a tile whose workgroup has not started after a bounded wait is claimed
+// and counted by workgroup 0 itself, so the launch cannot deadlock however few
+// workgroups are resident), builds the tree (tree_body<true>) and publishes the code
+// table. Each packing workgroup then takes its own tile's bit count (its counts x code
+// lengths), publishes it, and sums every earlier tile's count in one round of loads for
+// its first bit -- instead of re-reading every earlier tile's histogram (the two-launch
+// path) or walking a look-back chain. The last workgroup to finish re-zeroes the launch
+// state and bumps the generation for the next frame.
+constexpr uint64_t kAggFlag = 1ull << 62, kValMask = (1ull << 62) - 1ull;
 #ifndef MH_ONE_CLAIM_TICKS  // workgroup 0's wait before it counts missing tiles itself (s_memrealtime, 100 MHz)
 #define MH_ONE_CLAIM_TICKS 2000  // 20 us
 #endif
@@ -1192,60 +1195,123 @@ __device__ __forceinline__ uint64_t tile_symbols(const Pixels px, uint64_t nb, u
   return q;
 }
 
-// Workgroup 0, before the tree: every tile's counts in hist.
+__device__ __forceinline__ uint32_t call_gen(const uint64_t *meta) {
+  return (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kGen]), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT) % 65535u) + 1u;
+}
+
+// Workgroup 0, before the tree: the frame's 256 symbol counts into hist (part 0).
+// Each packing workgroup publishes its tile's counts as 128 u64 words of two tagged
+// counts (gen << 16 | count), one relaxed atomic store each: a word is valid when its
+// tags equal this call's generation, so there is no flag to order and no release (a
+// release fence writes the XCD's whole L2 back) and nothing to zero between calls.
+// Workgroup 0 first waits (bounded) on a published-tiles hint counter; tiles whose
+// workgroups have not claimed them by then are claimed and counted here (the launch
+// cannot deadlock however few workgroups are resident); then it sums every other
+// tile's words, 8 loads in flight per thread, waiting on any word not yet valid.
 __device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *hist,
-                                                uint64_t *meta, uint32_t *claim, uint32_t *h) {
-  __shared__ uint32_t s_next, s_mine;
-  const uint32_t tid = threadIdx.x;
+                                                uint64_t *meta, uint32_t *claim, const uint64_t *thw,
+                                                uint32_t *h) {
+  __shared__ uint32_t s_done, s_mine, s_list[MH_FUSED_MAX_TILES], s_own[256];
+  __shared__ uint32_t s_mask[(MH_FUSED_MAX_TILES + 31) / 32];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t gen = call_gen(meta);
+  if (tid < 256) s_own[tid] = 0;
+  if (tid < (MH_FUSED_MAX_TILES + 31) / 32) s_mask[tid] = 0;
   if (tid == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT) < ntiles &&
+    uint32_t d;
+    while ((d = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT)) < ntiles &&
            __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)MH_ONE_CLAIM_TICKS)
       __builtin_amdgcn_s_sleep(2);
+    s_done = d >= ntiles ? 1u : 0u;
     s_mine = 0;
-    s_next = 0;
   }
   __syncthreads();
-  // tiles nobody has claimed yet: count them here (rare; the packer that starts later
-  // finds its claim taken and leaves the histogram alone)
-  for (;;) {
-    if (tid == 0) {
-      uint32_t t = s_next;
-      for (; t < ntiles; ++t) {
-        uint32_t z = 0;
-        if (__hip_atomic_load(&claim[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-            __hip_atomic_compare_exchange_strong(&claim[t], &z, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-          break;
+  if (!s_done) {
+    // Rare: wave 0 tries to claim every unclaimed tile (64 claims at once); the packer
+    // that starts later finds its claim taken and publishes nothing. The whole
+    // workgroup counts the claimed tiles into s_own.
+    if (tid < 64) {
+      uint32_t k = 0;  // tiles claimed so far (the same in every lane)
+      for (uint32_t base = 0; base < ntiles; base += 64) {
+        const uint32_t t = base + lane;
+        bool got = false;
+        if (t < ntiles && __hip_atomic_load(&claim[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+          uint32_t z = 0;
+          got = __hip_atomic_compare_exchange_strong(&claim[t], &z, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint64_t m = __ballot(got);
+        if (got) {
+          s_list[k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = t;
+          atomicOr(&s_mask[t >> 5], 1u << (t & 31u));
+        }
+        k += (uint32_t)__popcll(m);
       }
-      s_next = t;
+      if (lane == 0) s_mine = k;
     }
     __syncthreads();
-    const uint32_t t = s_next;
-    if (t >= ntiles) break;
-    for (uint32_t i = tid; i < 256 * kHistCopies; i += kCodeThreads) h[i] = 0;
-    __syncthreads();
-    uint32_t first_unused;
-    tile_symbols(px, nb, t, h, &first_unused);
+    const uint32_t mine = s_mine;
+    for (uint32_t i = 0; i < mine; ++i) {
+      const uint32_t t = s_list[i];
+      for (uint32_t j = tid; j < 256 * kHistCopies; j += kCodeThreads) h[j] = 0;
+      __syncthreads();
+      uint32_t first_unused;
+      tile_symbols(px, nb, t, h, &first_unused);
+      __syncthreads();
+      if (tid < 256) {
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
+        s_own[tid] += c;
+      }
+      __syncthreads();
+    }
+  }
+  // every tile not counted here: its words, once tagged with this generation
+  {
+    const uint32_t col = tid & 127u, grp = tid >> 7;  // bins 2col, 2col+1; tiles grp, grp + 8, ...
+    const uint32_t tag = gen << 16;
+    uint32_t c0 = 0, c1 = 0;
+    for (uint32_t t0 = grp; t0 < ntiles; t0 += 8u * 8u) {
+      uint64_t v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t t = t0 + 8u * k;
+        v[k] = t < ntiles ? __hip_atomic_load(&thw[(uint64_t)t * 128 + col], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : 0ull;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t t = t0 + 8u * k;
+        if (t >= ntiles || ((s_mask[t >> 5] >> (t & 31u)) & 1u)) continue;
+        uint64_t x = v[k];
+        while (((uint32_t)x & 0xFFFF0000u) != tag || ((uint32_t)(x >> 32) & 0xFFFF0000u) != tag) {
+          __builtin_amdgcn_s_sleep(1);
+          x = __hip_atomic_load(&thw[(uint64_t)t * 128 + col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        c0 += (uint32_t)x & 0xFFFFu;
+        c1 += (uint32_t)(x >> 32) & 0xFFFFu;
+      }
+    }
+    __syncthreads();  // h is free again
+    h[grp * 256 + 2 * col] = c0;
+    h[grp * 256 + 2 * col + 1] = c1;
     __syncthreads();
     if (tid < 256) {
-      uint32_t c = 0;
-      for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
-      if (c) atomicAdd((unsigned long long *)&hist[(t % kHistParts) * 256 + tid], (unsigned long long)c);
+      uint64_t f = s_own[tid];
+#pragma unroll
+      for (uint32_t g = 0; g < 8; ++g) f += h[g * 256 + tid];
+      hist[tid] = f;  // part 0; the tree reads (and re-zeroes) every part
     }
-    if (tid == 0) {
-      ++s_mine;
-      ++s_next;
-    }
-    __syncthreads();
-  }
-  // then the tiles whose own workgroups claimed them: all of their adds published
-  if (tid == 0) {
-    while (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT) + s_mine < ntiles)
-      __builtin_amdgcn_s_sleep(2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with each packer's release increment
+    // words of tiles counted here stay stale: clear them so a later generation with the
+    // same tag (65535 calls on) cannot mistake them
+    if (s_mine)
+      for (uint32_t i = 0; i < s_mine; ++i)
+        if (tid < 128) __hip_atomic_store((uint64_t *)&thw[(uint64_t)s_list[i] * 128 + tid], 0ull, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
@@ -1272,13 +1338,14 @@ __device__ __forceinline__ void finish_launch(uint64_t *meta, uint64_t *tstate, 
   if (tid == 0) {
     for (uint32_t k : {kHistDone, kFlag, kAbort, kDone})
       __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[k]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kGen]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint64_t *hist, const uint32_t *table,
                                               uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint64_t nb,
                                               uint32_t ntiles, uint32_t *offsets, uint32_t *words, int32_t *status,
-                                              uint32_t *h, uint8_t *block_init) {
+                                              uint32_t *h, uint8_t *block_init, uint64_t *thw) {
   __shared__ uint32_t tab[256];
   __shared__ uint32_t lw[kCodeWords];
   __shared__ uint32_t s_cnt[256];
@@ -1287,6 +1354,13 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
   const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
   const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
   const bool on = b < nb;
+  MH_CODE_STAMP(t + 1, 0)
+  bool claimed = false;
+  if (tid == 0) {  // this tile's counts are published unless workgroup 0 took the tile over
+    uint32_t z = 0;
+    claimed = __hip_atomic_compare_exchange_strong(&claim[t], &z, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (uint32_t i = tid; i < 256 * kHistCopies; i += kCodeThreads) h[i] = 0;
   // (lanes 0-7, t > 0) the previous block's rows: the head bits of this tile's first word
   const uint64_t gp = (t > 0 && tid < 8) ? block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
@@ -1301,20 +1375,19 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
     for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
     s_cnt[tid] = c;
   }
-  if (tid == 0) {  // this tile's counts go into hist unless workgroup 0 took the tile over
-    uint32_t z = 0;
-    s_flag = __hip_atomic_compare_exchange_strong(&claim[t], &z, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
-  }
+  if (tid == 0) s_flag = claimed ? 1u : 0u;
   __syncthreads();
   const bool mine = s_flag != 0;
-  if (mine && tid < 256 && s_cnt[tid])
-    atomicAdd((unsigned long long *)&hist[(t % kHistParts) * 256 + tid], (unsigned long long)s_cnt[tid]);
-  __syncthreads();  // every add of this workgroup happens-before thread 0's release below
+  if (mine && tid < 128) {  // this tile's counts as tagged words (see wait_histograms)
+    const uint32_t tag = call_gen(meta) << 16;
+    const uint64_t w = (uint64_t)(tag | s_cnt[2 * tid]) | ((uint64_t)(tag | s_cnt[2 * tid + 1]) << 32);
+    __hip_atomic_store(&thw[(uint64_t)t * 128 + tid], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (tid == 0) {
-    if (mine)
-      __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 1u, __ATOMIC_RELEASE,
+    if (mine)  // a hint for workgroup 0's wait only: the words carry their own validity
+      __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+    MH_CODE_STAMP(t + 1, 1)
     // the code table (workgroup 0): relaxed polls, then one acquire fence
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t f;
@@ -1328,6 +1401,7 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     s_flag = f;
+    MH_CODE_STAMP(t + 1, 2)
   }
   __syncthreads();
   const uint32_t f = s_flag;
@@ -1353,32 +1427,44 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
     const uint32_t incl = wave_scan_dpp(nbits);
     if (lane == 63) s_scan[wave] = incl;
     __syncthreads();
-    if (tid == 0) {
-      // decoupled look-back: publish the aggregate, sum the tiles before this one
-      // back to the first published inclusive prefix, publish the inclusive prefix
+    if (wave == 0) {
+      // This tile's first bit = the sum of every earlier tile's bit count. Each tile
+      // publishes its count (one 64-bit word, flag and value together, so relaxed
+      // atomics suffice) as soon as the table is out; wave 0 then reads all earlier
+      // counts at once (<= 8 loads in flight per lane: one round trip) -- no serial
+      // look-back chain. A tile that never publishes (its workgroup gave up) times out
+      // this one too.
       const uint64_t agg = (uint64_t)s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
-      uint64_t E = 0;
-      bool ok = true;
-      if (t > 0) {
-        __hip_atomic_store(&tstate[t], kAggFlag | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (uint32_t u = t - 1; ok; --u) {
-          uint64_t v;
-          while (((v = __hip_atomic_load(&tstate[u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0u) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // a tile before gave up: so do we
-              ok = false;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          E += v & kValMask;
-          if ((v >> 62) == 2u) break;
-        }
+      if (lane == 0)
+        __hip_atomic_store(&tstate[t], kAggFlag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t v[MH_FUSED_MAX_TILES / 64];
+#pragma unroll
+      for (uint32_t k = 0; k < MH_FUSED_MAX_TILES / 64; ++k) {
+        const uint32_t u = lane + 64u * k;
+        v[k] = u < t ? __hip_atomic_load(&tstate[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kAggFlag;
       }
-      if (ok) __hip_atomic_store(&tstate[t], kInclFlag | (E + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      s_E = (uint32_t)E;
-      s_flag = ok ? 1u : 3u;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool lane_ok = true;
+      uint64_t x = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < MH_FUSED_MAX_TILES / 64; ++k) {
+        const uint32_t u = lane + 64u * k;
+        while (lane_ok && (v[k] >> 62) == 0u) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) lane_ok = false;
+          __builtin_amdgcn_s_sleep(1);
+          v[k] = __hip_atomic_load(&tstate[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        x += u < t ? (v[k] & kValMask) : 0ull;
+      }
+      for (uint32_t o = 32; o; o >>= 1) x += __shfl_xor(x, o);
+      const bool ok = __ballot(!lane_ok) == 0;
+      if (lane == 0) {
+        s_E = (uint32_t)x;
+        s_flag = ok ? 1u : 3u;
+      }
+      MH_CODE_STAMP(t + 1, 3)
     }
+    __syncthreads();
     if (wave == 0) {
       const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
       if (lane < kCodeWaves) s_scan[lane] = v;
@@ -1438,23 +1524,30 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
     if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
   }
 finish:
+#if MH_CODE_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  MH_CODE_STAMP(t + 1, 4)
+#endif
   finish_launch(meta, tstate, claim, ntiles, kCodeThreads);
 }
 
 __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kernel(
     uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta, uint64_t *codes_len_out, uint64_t codes_cap,
     int32_t *status, const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *tstate, uint32_t *claim,
-    uint32_t *offsets, uint32_t *words, uint8_t *block_init) {
+    uint32_t *offsets, uint32_t *words, uint8_t *block_init, uint64_t *thw) {
   __shared__ uint32_t s_h[256 * kHistCopies];  // one tile's symbol counts, kHistCopies copies
   if (blockIdx.x == 0) {
-    wait_histograms(px, nb, ntiles, hist, meta, claim, s_h);
+    MH_CODE_STAMP(0, 0)
+    wait_histograms(px, nb, ntiles, hist, meta, claim, thw, s_h);
+    MH_CODE_STAMP(0, 1)
     tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
+    MH_CODE_STAMP(0, 2)
     // tree_body ends with the 256 symbol threads (the other waves have exited)
     finish_launch(meta, tstate, claim, ntiles, 256);
     return;
   }
   pack_tile_one(blockIdx.x - 1, px, hist, table, meta, tstate, claim, nb, ntiles, offsets, words, status, s_h,
-                block_init);
+                block_init, thw);
 }
 
 }  // namespace
@@ -1528,7 +1621,9 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
   // the tree zeroes the histogram after reading it and the one-launch path's last
   // workgroup its state, for the next call
-  const size_t state_bytes = align256((kDone + 1) * 8) + align256(ncode * 8) + align256(ncode * 4);
+  // meta .. claim .. tile_hist are contiguous (carve)
+  const size_t state_bytes =
+      align256((kGen + 1) * 8) + align256(ncode * 8) + align256(ncode * 4) + align256(ncode * 256 * 4);
   if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) &&
       (hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess ||
        hipMemsetAsync(w.meta, 0, state_bytes, s) != hipSuccess))
@@ -1540,7 +1635,8 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
     const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
     hipLaunchKernelGGL(enc_one_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist, d_canon_header,
                        w.table, w.meta, d_codes_len, codes_cap, d_status, px, nb, (uint32_t)ncode, w.tstate, w.claim,
-                       d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), d_block_init);
+                       d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), d_block_init,
+                       reinterpret_cast<uint64_t *>(w.tile_hist));
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   if (ncode <= MH_FUSED_MAX_TILES && path == 2) {

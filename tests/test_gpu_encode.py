@@ -357,3 +357,38 @@ def test_encoder_alternative_paths(mh, path):
     env = dict(os.environ, MH_ENCODE_KERNELS=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_one_launch_claim_fallback(mh):
+    """The one-launch encoder's deadlock guard: workgroup 0 counts the tiles whose own
+    workgroups have not published their counts when its wait ends. A diagnostic build
+    with no wait at all (MH_ONE_CLAIM_TICKS=0) takes that path on most tiles of every
+    frame; the bytes must not change (child process, MH_LIB)."""
+    import os
+    import subprocess
+    import sys
+
+    import metalhuffman_amd.build as B
+    lib = B.diag_lib_path("claim0")
+    assert os.path.exists(lib), "build() makes the diagnostic libraries"
+    code = (
+        "import sys, numpy as np, torch; sys.path.insert(0, %r)\n"
+        "import metalhuffman_amd as mh\n"
+        "from metalhuffman_amd import frames as F\n"
+        "from metalhuffman_amd.encoder import Encoder\n"
+        "assert mh.lib().mh_build_stamp().decode().startswith('diag:claim0:')\n"
+        "bb = F.bigbridge()\n"
+        "for img, init in ((bb, False), (np.ascontiguousarray(bb[:777, :1001]), True)):\n"
+        "    ref = mh.encode_frame(img, init_zero_delta=init)\n"
+        "    enc = Encoder(img.shape[1], img.shape[0], 'cuda:0')\n"
+        "    for _ in range(3):\n"
+        "        a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).to('cuda:0'), 0, init)\n"
+        "        r = a.result()\n"
+        "        assert np.array_equal(r.canon, ref.canon)\n"
+        "        assert np.array_equal(r.codes.cpu().numpy(), ref.codes)\n"
+        "        assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)\n"
+        "        if init: assert np.array_equal(a.block_init.cpu().numpy(), ref.block_init)\n"
+        "print('ok')\n" % B.ROOT)
+    env = dict(os.environ, MH_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
