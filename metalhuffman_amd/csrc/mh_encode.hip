@@ -1227,6 +1227,7 @@ __device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, ui
       __builtin_amdgcn_s_sleep(2);
     s_done = d >= ntiles ? 1u : 0u;
     s_mine = 0;
+    MH_CODE_STAMP(0, 3)
   }
   __syncthreads();
   if (!s_done) {
@@ -1297,6 +1298,7 @@ __device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, ui
       }
     }
     __syncthreads();  // h is free again
+    MH_CODE_STAMP(0, 4)
     h[grp * 256 + 2 * col] = c0;
     h[grp * 256 + 2 * col + 1] = c1;
     __syncthreads();
@@ -1397,7 +1399,7 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
         f = 3u;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(16);  // ~0.45 us: 384 pollers on one word slow every other atomic
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     s_flag = f;
@@ -1554,15 +1556,17 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kerne
 
 extern "C" {
 
-// MH_ENCODE_KERNELS=4 selects the four-kernel path (split, tree, scan, pack) for
-// every frame size, =2 the two-launch path (split, then tree + packing with every
-// earlier tile's histogram summed per tile) -- A/B and tests. By default frames of
-// <= MH_FUSED_MAX_TILES code tiles take the one-launch path (enc_one_kernel), larger
-// ones the four-kernel path (workgroup 0 would count many non-resident tiles alone).
+// Frames of <= MH_FUSED_MAX_TILES code tiles take the two-launch path by default
+// (enc_split_kernel tiled, then enc_code_kernel: the tree in workgroup 0 while the
+// packers sum the earlier tiles' histograms). MH_ENCODE_KERNELS=1 selects the
+// one-launch path (enc_one_kernel: pixels read once, 0.6x the PMC traffic, but its
+// cross-XCD exchanges sit on the critical path: 3x slower, profiles/r03_encoder_one_launch_ab.txt),
+// =4 the four-kernel path (split, tree, scan, pack) for every size; larger frames
+// always take the four-kernel path.
 static int encode_kernels() {
   static const int k = [] {
     const char *v = std::getenv("MH_ENCODE_KERNELS");
-    return v ? std::atoi(v) : 1;
+    return v ? std::atoi(v) : 2;
   }();
   return k;
 }

@@ -4,7 +4,8 @@ Needs a library built with -DMH_CODE_STAMPS=1, loaded through MH_LIB:
     python -c "import metalhuffman_amd.build as B; B.build_variant('encstamps', ['MH_CODE_STAMPS=1'])"
     MH_LIB=ab/lib_encstamps.so python scripts/enc_one_stamps.py
 
-Workgroup 0: [0] start, [1] every tile's counts in, [2] table published.
+Workgroup 0: [0] start, [3] hint counter complete, [4] tagged words summed, [1] every
+tile's counts in, [2] table published.
 Packing workgroup t+1: [0] start, [1] counts published, [2] table seen, [3] first bit
 known (look-back), [4] tile written. Times in us from the earliest start (s_memrealtime,
 100 MHz)."""
@@ -38,6 +39,7 @@ for rep in range(4):
     w0 = a[0]
     pk = a[1:]
     pct = lambda v: "p0 %.1f p50 %.1f p100 %.1f" % (np.min(v), np.median(v), np.max(v))
-    print(f"rep {rep}: wg0 start {us(w0[0]):.1f} counts-in {us(w0[1]):.1f} table {us(w0[2]):.1f} | "
+    print(f"rep {rep}: wg0 start {us(w0[0]):.1f} hint-done {us(w0[3]):.1f} words-summed {us(w0[4]):.1f} "
+          f"counts-in {us(w0[1]):.1f} table {us(w0[2]):.1f} | "
           f"packers start [{pct(us(pk[:, 0]))}] published [{pct(us(pk[:, 1]))}] table-seen "
           f"[{pct(us(pk[:, 2]))}] lookback [{pct(us(pk[:, 3]))}] written [{pct(us(pk[:, 4]))}]")

@@ -27,7 +27,7 @@ for d in sorted(glob.glob(os.path.join(root, "*_*_SIZE"))):
             if r["Counter_Name"] != ctr:
                 continue
             if wl == "encode":  # per kernel of the encoder
-                for k in ("enc_split_kernel", "enc_code_kernel"):
+                for k in ("enc_split_kernel", "enc_code_kernel", "enc_one_kernel"):
                     if k in kn:
                         enc.setdefault(k, {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
             elif "mh_decode_kernel" in kn or "mh_decode_small_kernel" in kn:

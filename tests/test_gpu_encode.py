@@ -57,8 +57,8 @@ def test_encode_8192_tile(mh, device, bigbridge):
 
 @pytest.mark.parametrize("hw", [(2048, 2048), (2056, 2048), (8, 65528), (2048, 1536)])
 def test_async_encode_fused_path_boundary(mh, device, bigbridge, hw):
-    """Frames of up to 512 tiles of 128 blocks take the one-launch path (enc_one_kernel),
-    larger ones the four-kernel path. (h, w) = (2048, 2048) is exactly
+    """Frames of up to 512 tiles of 128 blocks take the two-launch path (tiled split +
+    code kernel), larger ones the four-kernel path. (h, w) = (2048, 2048) is exactly
     512 tiles, (2056, 2048) 514, (8, 65528) one block row of 8191 blocks (64 tiles,
     the last partial), (2048, 1536) BigBridge's shape transposed. Both sides
     byte-identical to the host codec."""
@@ -291,7 +291,8 @@ def test_async_encode_workspace_flag(mh, device, bigbridge):
         assert np.array_equal(r.canon, ref.canon) and np.array_equal(r.codes.cpu().numpy(), ref.codes), k
 
 
-def test_fused_encoder_timeout_is_sticky(mh):
+@pytest.mark.parametrize("path", ["2", "1"])
+def test_fused_encoder_timeout_is_sticky(mh, path):
     """A packing workgroup that gives up waiting for the code table (diagnostic build
     with a zero spin budget, MH_DIAG_SPIN_TICKS=0) must leave MH_ERR_HIP in the status,
     whenever workgroup 0's own status store lands (mh_encode.hip: meta[kAbort], all
@@ -321,17 +322,17 @@ def test_fused_encoder_timeout_is_sticky(mh):
         "        bad += 1\n"
         "print('timeouts', bad)\n"
         "assert bad == 4\n" % B.ROOT)
-    env = dict(os.environ, MH_LIB=lib)
+    env = dict(os.environ, MH_LIB=lib, MH_ENCODE_KERNELS=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("path", ["2", "4"])
+@pytest.mark.parametrize("path", ["1", "4"])
 def test_encoder_alternative_paths(mh, path):
-    """The one-launch path is the default for frames of <= 512 code tiles; the two-launch
-    (MH_ENCODE_KERNELS=2: tiled split + code kernel) and four-kernel (=4) paths stay
-    selectable and byte-identical to the host codec. The knob is read once per process,
-    so each path runs in a child process."""
+    """The two-launch path is the default for frames of <= 512 code tiles; the one-launch
+    (MH_ENCODE_KERNELS=1: enc_one_kernel) and four-kernel (=4) paths stay selectable and
+    byte-identical to the host codec. The knob is read once per process, so each path
+    runs in a child process."""
     import os
     import subprocess
     import sys
@@ -389,6 +390,6 @@ def test_one_launch_claim_fallback(mh):
         "        assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)\n"
         "        if init: assert np.array_equal(a.block_init.cpu().numpy(), ref.block_init)\n"
         "print('ok')\n" % B.ROOT)
-    env = dict(os.environ, MH_LIB=lib)
+    env = dict(os.environ, MH_LIB=lib, MH_ENCODE_KERNELS="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
