@@ -43,7 +43,11 @@ constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is publis
 constexpr uint32_t kAbort = 19;         // meta[] slot: a packing workgroup gave up waiting (fused path)
 constexpr uint32_t kHistDone = 20;      // meta[] slot: tiles whose counts are in hist (one-launch path)
 constexpr uint32_t kDone = 21;          // meta[] slot: packing workgroups finished (one-launch path)
-constexpr uint32_t kGen = 22;           // meta[] slot: the one-launch path's call generation (1..65535)
+constexpr uint32_t kGen = 22;           // meta[] slot: call generation of the fused paths (table tags, count tags)
+#ifndef MH_DIAG_SPIN_TICKS  // diagnostic builds only (tests/test_gpu_encode.py: forced timeout)
+#define MH_DIAG_SPIN_TICKS 10000000
+#endif
+constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;  // a packer's wait limit: 100 ms of s_memrealtime (100 MHz)
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 #ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
 #define MH_FUSED_MAX_TILES 512
@@ -178,6 +182,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   if (tiled && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
     meta[kFlag] = 0;
     meta[kAbort] = 0;
+    meta[kGen] += 1;  // a new tag for the code table words (table_tag)
   }
   MH_SPLIT_STAMP(0)
   __shared__ uint32_t h[256 * kHistCopies];
@@ -337,6 +342,42 @@ template <uint32_t K = 2>
 __device__ __forceinline__ void wave_sort64(uint32_t lane, uint32_t &key) {
   sort_merge<K, K / 2>(lane, key);
   if constexpr (K < 64) wave_sort64<K * 2>(lane, key);
+}
+
+// The fused paths' call tag (1..255) in the code table words: from meta[kGen], which
+// the split kernel (two-launch path) or the last workgroup of the previous launch
+// (one-launch path) advances once per call.
+__device__ __forceinline__ uint32_t table_tag(const uint64_t *meta) {
+  return (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kGen]), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT) % 255u) + 1u;
+}
+
+// A packing workgroup's wait for the code table: threads 0-255 poll their own word
+// until it carries this call's tag, then keep code | length in `tab`. Returns 1 (table
+// in tab), 2 (a rejected frame: the tree set the bad bit) or 3 (timed out).
+__device__ __forceinline__ uint32_t wait_table(const uint32_t *table, const uint64_t *meta, uint32_t *tab,
+                                               uint32_t sleep_after) {
+  const uint32_t tid = threadIdx.x;
+  bool timeout = false, bad = false;
+  if (tid < 256) {
+    const uint32_t tag = table_tag(meta);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t w;
+    uint32_t polls = 0;
+    while (((w = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 8 & 0xFFu) != tag) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
+        timeout = true;
+        break;
+      }
+      if (++polls > sleep_after) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(1);
+    }
+    tab[tid] = w & 0xFFFF001Fu;  // code (left-justified, 16 bits) << 16 | length
+    bad = (w & 0x80u) != 0u;
+  }
+  const bool any_timeout = __syncthreads_or(timeout) != 0;
+  const bool any_bad = __syncthreads_or(bad) != 0;
+  return any_timeout ? 3u : any_bad ? 2u : 1u;
 }
 
 // One 256-thread workgroup: the reference's Huffman tree (HuffmanEncoder.cpp:29-145)
@@ -659,16 +700,15 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     for (uint32_t w = 0; w < wave; ++w) rank += s_wcnt[w][L];
     e = ((((s_first[L] + rank) << (16 - L)) & 0xFFFFu) << 16) | L;
   }
-  if constexpr (kFused)
-    __hip_atomic_store(&table[tid], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    table[tid] = e;
+  if constexpr (!kFused) table[tid] = e;
+  __shared__ uint32_t s_bad2;
   uint32_t published = 0;
   if (tid == 0) {
     const uint64_t total = s_total;
     const uint64_t len = (total + 7) / 8 + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
     uint32_t bad = s_bad;
     if (!bad && (total >= (1ull << 32) || ((len + 3) & ~3ull) > codes_cap)) bad = (uint32_t)-MH_ERR_CAPACITY;
+    s_bad2 = bad;
     meta[0] = bad ? 0 : len;
     meta[1] = bad ? 0 : 1;
     meta[kTicket] = 0;
@@ -690,16 +730,16 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     published = bad ? 2u : 1u;
   }
   if constexpr (kFused) {
-    // Publication in the HIP memory model: every thread's table store (an agent-scope
-    // atomic) happens-before thread 0's flag store through the workgroup barrier, and
-    // the flag store is an agent-scope release that the packers' acquire pairs with
-    // (pack_tile): release/acquire, no reliance on vmcnt ordering.
-    MH_CODE_STAMP(0, 1)
+    // Publication: each table word carries this call's tag (bits 8-15) and, for a
+    // rejected frame, the bad bit (7): a packing workgroup polls the words themselves,
+    // each valid on its own -- one relaxed agent-scope atomic per word, no flag to order
+    // against the table (no release/acquire pair, no vmcnt reliance) and no second
+    // round trip for the table after the flag.
     __syncthreads();
-    MH_CODE_STAMP(0, 2)
-    if (tid == 0)
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kFlag]), published, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag = table_tag(meta);
+    __hip_atomic_store(&table[tid], e | (tag << 8) | (s_bad2 ? 0x80u : 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    MH_CODE_STAMP(0, 1)
   }
   (void)published;
   MH_TREE_STAMP(8);
@@ -935,10 +975,6 @@ constexpr uint32_t kCodeThreads = 1024;
 #endif
 constexpr uint32_t kCodeWaves = kCodeThreads / 64;
 constexpr uint32_t kCodeWords = kCodeTile * 64 * 16 / 32 + 2;  // a tile's code words, <= 16-bit codes
-#ifndef MH_DIAG_SPIN_TICKS  // diagnostic builds only (tests/test_gpu_encode.py: forced timeout)
-#define MH_DIAG_SPIN_TICKS 10000000
-#endif
-constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;             // 100 ms of s_memrealtime (100 MHz)
 static_assert(kCodeThreads == 8 * kCodeTile, "eight lanes per block");
 
 // Inclusive prefix sum over the wave by DPP (row_shr 1/2/4/8 inside each row of 16
@@ -976,7 +1012,6 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
   __shared__ uint32_t lw[kCodeWords];
   __shared__ uint32_t s_cnt[kCodeWaves][256];  // symbol counts of the tiles before this one, per wave
   __shared__ uint32_t s_dot[4], s_scan[kCodeWaves];
-  __shared__ uint32_t s_flag;
   const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
   MH_CODE_STAMP(t + 1, 0)
   const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
@@ -1025,25 +1060,8 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
   uint32_t first_unused;
   const uint64_t q = row_symbols(gq, part, px.delta, px.init_byte, &first_unused);
   const uint64_t qp = row_symbols(gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // used by lanes 0-7 of wave 0
-  if (tid == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t f;
-    // relaxed polls (an acquire per poll would invalidate caches on every iteration),
-    // then one agent-scope acquire fence once the flag is seen
-    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
-        f = 3u;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the tree's release store
-    s_flag = f;
-  }
+  const uint32_t f = wait_table(table, meta, tab, 64);  // tagged words: see tree_body
   MH_CODE_STAMP(t + 1, 1)
-  __syncthreads();
-  const uint32_t f = s_flag;
   if (f != 1u) {  // rejected frame (status set by the tree): write nothing
     if (f == 3u && tid == 0) {  // timed out: sticky, whenever the tree's own status lands
       __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST,
@@ -1052,10 +1070,6 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
     }
     return;
   }
-  // thread 0's acquire reaches the table readers through the workgroup barrier above
-  // (happens-before is transitive), and the table loads are agent-scope atomics
-  if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
   MH_CODE_STAMP(t + 1, 2)
   // E = first bit of this tile = sum over symbols of (count before the tile) x length
   if (wave < 4) {
@@ -1390,26 +1404,10 @@ __device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint6
       __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     MH_CODE_STAMP(t + 1, 1)
-    // the code table (workgroup 0): relaxed polls, then one acquire fence
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t f;
-    while ((f = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kFlag]), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // exit condition: never hang
-        f = 3u;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(16);  // ~0.45 us: 384 pollers on one word slow every other atomic
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    s_flag = f;
-    MH_CODE_STAMP(t + 1, 2)
   }
-  __syncthreads();
-  const uint32_t f = s_flag;
+  const uint32_t f = wait_table(table, meta, tab, 16);  // tagged words: see tree_body
+  MH_CODE_STAMP(t + 1, 2)
   if (f == 1u) {
-    if (tid < 256) tab[tid] = __hip_atomic_load(&table[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
     // this tile's bit count: its counts x code lengths
     if (wave < 4) {
       const uint32_t x = wave_scan_dpp(s_cnt[tid] * (tab[tid] & 0xFFu));
