@@ -177,22 +177,35 @@ class Workload:
             self.launch(i)
         torch.cuda.synchronize(dev)
         # Long launches (>= LONG_LAUNCH_PIXELS decoded per launch: the 64-frame batch, the
-        # 8192^2 frame; 20-70 us each) are timed as plain eager launches: the host enqueues
-        # them faster than they run, so the queue never drains and no gate or graph is
-        # needed (a hipGraph replay of 256 such launches cost the host ~2x the GPU time,
-        # and under rocprofv3 a long graph queued behind the gate ran 13-17 % slower per
-        # dispatch than the same launches plainly: profiles/r03_gate_rocprof_artifact.txt).
-        # Short launches (one 2048x1536 frame, ~5.5 us) are queued behind the launch gate.
+        # 8192^2 frame; 20-70 us each) replay a graph of LONG_GRAPH_LAUNCHES launches
+        # K / LONG_GRAPH_LAUNCHES times behind the launch gate: one graph of all K queued
+        # behind the gate ran 13-17 % slower per dispatch under rocprofv3 than the same
+        # launches unprofiled (profiles/r03_gate_rocprof_artifact.txt), and plain eager
+        # regions dispatch 5-8 % slower than queued ones (profiles/r03_long_launch_ab.txt).
+        # A launch of >= 113 MB leaves nothing warm in the 256 MiB Infinity Cache for the
+        # next replay of the same sequence. Short launches (one 2048x1536 frame, ~5.5 us)
+        # keep one graph of the K distinct launches (or eager launches behind the gate).
         # Decided by size, not by a timing probe: under a profiler the probe itself slows.
         self.long_launches = self.pixels >= LONG_LAUNCH_PIXELS
-        if self.long_launches:
+        mode = os.environ.get("MH_BENCH_LONG", "graph")
+        if self.long_launches and mode == "eager":
             use_graph = gate = False
+        if self.long_launches and mode == "graph_ungated":  # A/B: the same replays, no gate
+            gate = False
+        G = steps  # launches per captured graph
+        if self.long_launches and mode.startswith("graph") and steps % LONG_GRAPH_LAUNCHES == 0:
+            G = LONG_GRAPH_LAUNCHES
+        self.graph_launches = G
         graph = None
+
+        def replay_all():  # the K launches: K / G replays of the G-launch graph
+            for _ in range(steps // G):
+                graph.replay()
         if use_graph:
             try:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    for i in range(steps):
+                    for i in range(G):
                         self.launch(i)
                 graph.replay()  # first replay off the clock (instantiation effects)
                 torch.cuda.synchronize(dev)
@@ -201,7 +214,7 @@ class Workload:
                 # 20-step graph measured 30-50 % slower than the median of many)
                 t_end = time.perf_counter() + settle_ms * 1e-3
                 while time.perf_counter() < t_end:
-                    graph.replay()
+                    replay_all()
                     torch.cuda.synchronize(dev)
             except Exception as e:  # pragma: no cover - fall back to eager launches
                 print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
@@ -212,7 +225,7 @@ class Workload:
             wa, wb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             wa.record()
             if graph is not None:
-                graph.replay()
+                replay_all()
             wb.record()
             torch.cuda.synchronize(dev)
             wa.elapsed_time(wb)
@@ -221,26 +234,28 @@ class Workload:
             if graph is not None and settle_ms:
                 t_end = time.perf_counter() + settle_ms * 1e-3
                 while time.perf_counter() < t_end:
-                    graph.replay()
+                    replay_all()
                     torch.cuda.synchronize(dev)
             wa, wb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize(dev)
             ta = time.perf_counter()
             wa.record()
-            graph.replay() if graph is not None else [self.launch(i) for i in range(steps)]
+            replay_all() if graph is not None else [self.launch(i) for i in range(steps)]
             wb.record()
             torch.cuda.synchronize(dev)
             print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
         # eager behind the gate for short regions only: there the replayed graph's ~6 us
         # start costs most; over 256 launches of the 64-frame batch the eager dispatches
         # ran 68.2 vs 63.6 us each (graph), so long regions keep the replay
-        eager_gated = GATED_EAGER and steps <= 64
+        eager_gated = GATED_EAGER and steps <= 64 and not self.long_launches
         def timed(gated, events=True, mark=False):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
             opening synchronize, and the clock starts when the host opens it -- every
             decode runs inside the region, the host's enqueue latency does not."""
             r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            rA = torch.cuda.Event(enable_timing=True)  # after the region's first launch (or replay)
+            unit = G if (graph is not None and not (gated and eager_gated)) else 1
             if dist.is_initialized():
                 dist.barrier()
             st = torch.cuda.current_stream(dev).cuda_stream
@@ -253,13 +268,18 @@ class Workload:
                 if events:
                     r0.record()
                 if graph is not None and not (gated and eager_gated):
-                    graph.replay()
+                    for r in range(steps // G):
+                        graph.replay()
+                        if r == 0 and events:
+                            rA.record()
                 else:
                     # any-order only when every launch of the region writes its own raster
                     # (no launch may overlap one that writes the same buffer)
                     relax = ANY_ORDER and len(self.launches) >= steps
                     for i in range(steps):
                         self.launch(i, relaxed=relax and i > 0)
+                        if i == 0 and events:
+                            rA.record()
                 if events:
                     r1.record()
             # (no barrier while a gate is armed: an RCCL barrier would queue behind it;
@@ -270,10 +290,19 @@ class Workload:
             else:
                 r0.record()
                 if graph is not None:
-                    graph.replay()
+                    for r in range(steps // G):
+                        graph.replay()
+                        if r == 0:
+                            rA.record()
                 else:
+                    # diagnostics only (MH_BENCH_DIAG_RELAX=1): launches 2..K without the
+                    # barrier bit even over one raster (identical bytes) -- the A/B of what
+                    # a plain dispatch's barrier costs
+                    diag_relax = os.environ.get("MH_BENCH_DIAG_RELAX", "0") == "1"
                     for i in range(steps):
-                        self.launch(i)
+                        self.launch(i, relaxed=diag_relax and i > 0)
+                        if i == 0:
+                            rA.record()
                 r1.record()
             if mark and GATE.ok():
                 GATE.marker(st, 2)  # after the last launch (one empty kernel inside a plain region's wall)
@@ -285,7 +314,12 @@ class Workload:
                 t = torch.tensor([w], dtype=torch.float64, device=on)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 w = float(t.item())
-            return w, (r0.elapsed_time(r1) if events else None)
+            self.steady_unit = unit
+            # steady-state launch time: the launches after the first unit (the first one also
+            # holds the gate's release and the first dispatch's start-up)
+            steady = (rA.elapsed_time(r1) / (steps - unit) if events and steps > unit else
+                      (r0.elapsed_time(r1) / steps if events else None))
+            return w, (r0.elapsed_time(r1) if events else None), steady
 
         if gate and GATE.ok():
             timed(True)  # the gate's own first launch off the clock
@@ -294,15 +328,16 @@ class Workload:
             # MB/s interleaved, profiles/r02_v13_region_events_ab.txt), so the event-timed
             # region is a second, identical one. MH_BENCH_REGION_EVENTS=1 keeps them inside.
             if os.environ.get("MH_BENCH_REGION_EVENTS", "0") == "0":
-                wall, _ = timed(True, events=False)
-                _, region_ms = timed(True, mark=True)
+                wall, _, _ = timed(True, events=False)
+                _, region_ms, steady_ms = timed(True, mark=True)
             else:
-                wall, region_ms = timed(True, mark=True)
-            self.ungated_wall, _ = timed(False)
+                wall, region_ms, steady_ms = timed(True, mark=True)
+            self.ungated_wall, _, _ = timed(False)
             self.timed_launch = (("eager behind the launch gate" + (", launches 2..K with MH_FLAG_ANY_ORDER" if ANY_ORDER else ""))
-                                 if eager_gated else "hipGraph behind the launch gate")
+                                 if eager_gated else
+                                 f"{steps // G} replays of a {G}-launch hipGraph behind the launch gate")
         else:
-            wall, region_ms = timed(False, mark=True)
+            wall, region_ms, steady_ms = timed(False, mark=True)
             self.ungated_wall = None
             self.timed_launch = ("hipGraph" if graph is not None else
                                  "eager (long launches: the host enqueues ahead of the GPU)"
@@ -312,7 +347,16 @@ class Workload:
         # cost of opening a region (gate release, first dispatch: ~13 us measured)
         # is amortised as in rocprofv3's per-dispatch durations of the same launches.
         self.region_kernel_ms = region_ms / steps
-        if graph is not None:
+        self.steady_kernel_ms = steady_ms
+        if graph is not None and G < steps:
+            ka, kb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            ka.record()
+            replay_all()
+            kb.record()
+            torch.cuda.synchronize(dev)
+            self.kernel_ms = ka.elapsed_time(kb) / steps
+        elif graph is not None:
             # one graph of >= 200 launches (a replayed graph's first kernel starts ~6 us
             # late: 10 replays of a 20-launch graph would add ~0.3 us per launch)
             kg, nk = graph, steps
@@ -345,7 +389,8 @@ class Workload:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
-LONG_LAUNCH_PIXELS = 16 << 20  # Workload.run: launches decoding this many pixels are timed as plain eager launches
+LONG_LAUNCH_PIXELS = 16 << 20  # Workload.run: launches decoding this many pixels are "long"
+LONG_GRAPH_LAUNCHES = 16       # ... and replay a graph of this many launches K / 16 times
 
 
 def measured_traffic(workload: str):
@@ -416,23 +461,28 @@ GATED_EAGER = os.environ.get("MH_BENCH_GATED_LAUNCH", "eager") == "eager"
 
 
 def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None, read_bytes=None,
-             kernel_ms=None):
+             kernel_ms=None, steady_ms=None, steady_unit=1):
     """achieved = algorithmic bytes of one launch / the launch's average duration,
-    the latter from the timed region itself: the HIP event pair on the launch stream
-    around the K timed launches, / K (kernel_us_avg). rocprofv3 --kernel-trace of the
-    same command reports per-dispatch durations that agree with it (back-to-back
-    dispatches: each one's start is its predecessor's end, so a run's durations sum to
-    its span; profiles/r03_ktrace_summary*.txt). graph_us_per_launch is the same
-    launches replayed as one graph of >= 200 (Workload.run), for reference.
+    the latter from the timed region itself, by HIP events on the launch stream:
+    kernel_us_avg = (end of the region - end of its first launch or first graph replay of
+    `steady_unit` launches) / (K - steady_unit), i.e. the back-to-back launch period inside
+    the region without the gate's release and the first dispatch's start-up (which
+    region_us_per_launch = the whole region / K still holds). rocprofv3 --kernel-trace of
+    the same command gives the same quantity from its dispatch timestamps
+    (scripts/ktrace_summary.py `timed_steady`; profiles/r03_ktrace_summary.txt).
+    graph_us_per_launch: the same launches replayed as graphs (Workload.run), for reference.
     frac is against the 8 TB/s spec; frac_of_achievable against a plain streaming
     kernel with the decoder's read:write mix measured on the same box."""
-    avg_s = region_ms / steps * 1e-3
+    avg_s = (steady_ms if steady_ms else region_ms / steps) * 1e-3
     ach = bytes_per_launch / avg_s / 1e9
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(ach / HBM_PEAK_GBS, 4),
          "traffic": measured_traffic(workload) if workload else None,
          "kernel_us_avg": round(avg_s * 1e6, 3),
-         "kernel_us_source": "HIP events around the timed region / K",
+         "kernel_us_source": (f"HIP events over the timed region after its first {steady_unit} launch(es), "
+                              f"/ (K - {steady_unit})" if steady_ms else "HIP events around the timed region / K"),
+         "kernel_us_steady_unit": steady_unit if steady_ms else 0,
+         "region_us_per_launch": round(region_ms * 1e3 / steps, 3),
          "graph_us_per_launch": round(kernel_ms * 1e3, 3) if kernel_ms else None,
          "algorithmic_bytes_per_launch": int(bytes_per_launch)}
     mix = ACHIEVABLE.get("mix_2r3w_GBps")
@@ -877,7 +927,7 @@ def main(argv=None) -> int:
                    "parallelism": f"frame-sharded x{world}", "launch": wl.timed_launch},
         "mpixels_per_s": round(value, 1),
         "roofline": roofline(wl.bytes, region_ms, args.steps, kms, args.workload, wl.read_bytes,
-                             wl.kernel_ms),
+                             wl.kernel_ms, wl.steady_kernel_ms, wl.steady_unit),
         "gpu_region_ms_per_step": round(region_ms / args.steps, 5),
         "timing": ("gated: the K launches are enqueued behind a host-opened launch gate before "
                    "the clock starts (scripts/micro/launch_gate.hip); every decode runs inside "
@@ -928,7 +978,7 @@ def main(argv=None) -> int:
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
                             "frames_verified": nver,
                             "roofline": roofline(w2.bytes, reg2, steps, kms2, key, w2.read_bytes,
-                                                 w2.kernel_ms)}
+                                                 w2.kernel_ms, w2.steady_kernel_ms, w2.steady_unit)}
             del w2
         extras["hbm_copy"] = copy_bandwidth(dev)  # achievable HBM rate beside the 8 TB/s spec
         if ACHIEVABLE:
@@ -952,7 +1002,8 @@ def main(argv=None) -> int:
             "frames_per_launch_per_gpu": int(b.launches[0].n_frames), "frames_total": world * int(b.launches[0].n_frames),
             "steps": bsteps, "value_MBps": round(world * b.pixels / (bwall / bsteps) / 1e6, 1),
             "ms_per_step": round(bwall / bsteps * 1e3, 4), "frames_verified_rank0": nver,
-            "roofline_rank0": roofline(b.bytes, breg, bsteps, bkms, "batch", b.read_bytes, b.kernel_ms)}
+            "roofline_rank0": roofline(b.bytes, breg, bsteps, bkms, "batch", b.read_bytes, b.kernel_ms,
+                                       b.steady_kernel_ms, b.steady_unit)}
         del b
         st = stream_h2d(efs, tables, dev, sync=dist.barrier)
         got = [None] * world

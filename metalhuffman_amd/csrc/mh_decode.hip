@@ -81,6 +81,9 @@ namespace {
 #ifndef MH_LUT_FIRST            // 1: batch kernel issues the table's loads before the first header (A/B)
 #define MH_LUT_FIRST 0
 #endif
+#ifndef MH_TLB_PREFETCH         // 1: the small kernel touches its code and raster pages at wave
+#define MH_TLB_PREFETCH 0       //    start, beside the block-offset load (translation warm-up, A/B)
+#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0
 #endif
@@ -813,6 +816,26 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr h;
   hdr_issue(a, tile, lane, h);
+#if MH_TLB_PREFETCH
+  // Translation warm-up: one load from the page of the code bytes this tile most likely
+  // starts in (its share of the frame's bytes; only the address's page matters, the
+  // value is never used) and one from its first raster row, issued beside the
+  // block-offset load so the three page walks overlap instead of following each other.
+  uint32_t warm = 0;
+  {
+    const uint32_t tf = a.total_tiles <= a.tiles_per_frame ? tile : tile % a.tiles_per_frame;
+    const uint32_t fb = (uint32_t)min<uint64_t>(a.codes_bytes, 0xFFFFFFF0ull);
+    const uint32_t est = (uint32_t)(((uint64_t)tf * fb) / a.tiles_per_frame) & ~63u;
+    const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(a.codes, a.frame_off ? 0u : fb);
+    const uint32_t by0 = (tf * 64u) / a.bw;
+    const uint64_t ro = (uint64_t)by0 * 8u * a.out_pitch;
+    const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(a.out, ro < a.out_frame_bytes ? 0x7FFFFFF0u : 0u);
+    if (lane == 0) {
+      warm = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)est, 0, 0);
+      warm += __builtin_amdgcn_raw_buffer_load_b32(rw, (int)(uint32_t)min<uint64_t>(ro, 0x7FFFFF00ull), 0, 0);
+    }
+  }
+#endif
   const bool l14 = max_len <= (uint32_t)kLut14Bits;
   // Table copy: a fixed count of unconditional 16-B loads per thread (chunks past
   // the table fall outside the descriptor), issued behind the offsets so that the
@@ -861,6 +884,9 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   } else {
     decode_halves<kDelta, StepCfg<kLutBits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
+#if MH_TLB_PREFETCH
+  if (warm == 0x9E3779B9u && lane == 64u) a.out[0] = 0;  // never true (lane < 64): keeps the loads
+#endif
 #if MH_DIAG_STAMPS
   MH_STAMP(4);
   ts[5] = ts[4];

@@ -17,7 +17,8 @@ for spec in frame:20:5 batch:256:256 tile8192:512:512 tile8192_random:512:512; d
   IFS=: read wl k w <<< "$spec"
   rm -rf $GRAFT_REPO_ROOT/gpurun_out/prof_$wl
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$wl -o run -- python3 bench.py --workload $wl --steps $k --warmup $w --no-extras --no-cpu-baseline > gpurun_out/bench_prof_$wl.json 2> gpurun_out/bench_prof_$wl.err || { tail gpurun_out/bench_prof_$wl.err; exit 1; }
-  { echo "== bench.py --workload $wl --steps $k --warmup $w (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"))"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl $k; } >> gpurun_out/ktrace_summary.txt
+  u=$(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline'].get('kernel_us_steady_unit') or 1)")
+  { echo "== bench.py --workload $wl --steps $k --warmup $w (profiled line: roofline.kernel_us_avg $(python3 -c "import json;print(json.load(open('gpurun_out/bench_prof_$wl.json'))['roofline']['kernel_us_avg'])"), steady unit $u)"; python3 scripts/ktrace_summary.py gpurun_out/prof_$wl $k $u; } >> gpurun_out/ktrace_summary.txt
 done
 cat gpurun_out/ktrace_summary.txt
 # producer side: the GPU encoder (async, back to back) and the device-only chain

@@ -9,7 +9,12 @@ region whose HIP events give kernel_us_avg: bench.py brackets exactly that regio
 two empty trace_marker_kernel launches (scripts/micro/launch_gate.hip), and the
 decode dispatches between the last pair of markers are taken.
 
-    python scripts/ktrace_summary.py gpurun_out/prof_frame [K]
+`timed_steady` = (end of the last of them - end of the first `unit`) / (K - unit): the
+same back-to-back launch period as the line's kernel_us_avg (bench.roofline; `unit` =
+the line's roofline.kernel_us_steady_unit: 1 for eager launches, 16 for long launches
+replayed as 16-launch graphs).
+
+    python scripts/ktrace_summary.py gpurun_out/prof_frame [K] [unit]
 """
 import collections
 import csv
@@ -19,6 +24,7 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+unit = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 groups = collections.defaultdict(list)
 markers = []
 for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
@@ -34,7 +40,7 @@ for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
 
 
 print(f"{'kernel':>8} {'grid_threads':>12} {'wg':>5} {'lds':>6} {'vgpr':>5} {'n':>5} {'avg_us':>9} "
-      f"{'median_us':>9} {'min_us':>8} {'timed_avg':>9} {'timed_span/K':>12}")
+      f"{'median_us':>9} {'min_us':>8} {'timed_avg':>9} {'timed_span/K':>12} {'timed_steady':>12}")
 for (k, g, w, lds, v), d in sorted(groups.items(), key=lambda kv: -len(kv[1])):
     d.sort()
     dur = [(e - s) / 1e3 for s, e in d]
@@ -47,5 +53,7 @@ for (k, g, w, lds, v), d in sorted(groups.items(), key=lambda kv: -len(kv[1])):
         timed = timed if len(timed) == steps else []
     ta = f"{statistics.mean((e - s) / 1e3 for s, e in timed):9.3f}" if timed else f"{'-':>9}"
     sp = f"{(timed[-1][1] - timed[0][0]) / 1e3 / len(timed):12.3f}" if timed else f"{'-':>12}"
+    ok = timed and len(timed) > unit
+    sd = f"{(timed[-1][1] - timed[unit - 1][1]) / 1e3 / (len(timed) - unit):12.3f}" if ok else f"{'-':>12}"
     print(f"{k:>8} {g:12d} {w:5d} {lds:6d} {v:5d} {n:5d} {statistics.mean(dur):9.3f} "
-          f"{statistics.median(dur):9.3f} {min(dur):8.3f} {ta} {sp}")
+          f"{statistics.median(dur):9.3f} {min(dur):8.3f} {ta} {sp} {sd}")

@@ -49,6 +49,11 @@ def test_roofline_fields_and_arithmetic(bench):
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     # the timed region's own events / K, not the 200-launch graph
     assert r["kernel_us_avg"] == pytest.approx(5.8, abs=1e-3)
+    assert r["region_us_per_launch"] == pytest.approx(5.8, abs=1e-3)
+    # with the steady-state figure (the region after its first launch) that one is used
+    r2 = bench.roofline(5_281_084, region_ms=0.116, steps=20, steady_ms=0.0055, steady_unit=1)
+    assert r2["kernel_us_avg"] == pytest.approx(5.5, abs=1e-3) and r2["kernel_us_steady_unit"] == 1
+    assert r2["region_us_per_launch"] == pytest.approx(5.8, abs=1e-3)
     assert r["achieved"] == pytest.approx(5_281_084 / 5.8e-6 / 1e9, rel=1e-3)
     assert r["frac"] == pytest.approx(r["achieved"] / 8000.0, abs=1e-4)
     assert r["frac_of_achievable"] == pytest.approx(r["achieved"] / 5800.0, abs=1e-4)
