@@ -314,12 +314,11 @@ class Workload:
                 t = torch.tensor([w], dtype=torch.float64, device=on)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 w = float(t.item())
-            self.steady_unit = unit
             # steady-state launch time: the launches after the first unit (the first one also
             # holds the gate's release and the first dispatch's start-up)
             steady = (rA.elapsed_time(r1) / (steps - unit) if events and steps > unit else
                       (r0.elapsed_time(r1) / steps if events else None))
-            return w, (r0.elapsed_time(r1) if events else None), steady
+            return w, (r0.elapsed_time(r1) if events else None), (steady, unit)
 
         if gate and GATE.ok():
             timed(True)  # the gate's own first launch off the clock
@@ -329,15 +328,15 @@ class Workload:
             # region is a second, identical one. MH_BENCH_REGION_EVENTS=1 keeps them inside.
             if os.environ.get("MH_BENCH_REGION_EVENTS", "0") == "0":
                 wall, _, _ = timed(True, events=False)
-                _, region_ms, steady_ms = timed(True, mark=True)
+                _, region_ms, (steady_ms, self.steady_unit) = timed(True, mark=True)
             else:
-                wall, region_ms, steady_ms = timed(True, mark=True)
+                wall, region_ms, (steady_ms, self.steady_unit) = timed(True, mark=True)
             self.ungated_wall, _, _ = timed(False)
             self.timed_launch = (("eager behind the launch gate" + (", launches 2..K with MH_FLAG_ANY_ORDER" if ANY_ORDER else ""))
                                  if eager_gated else
                                  f"{steps // G} replays of a {G}-launch hipGraph behind the launch gate")
         else:
-            wall, region_ms, steady_ms = timed(False, mark=True)
+            wall, region_ms, (steady_ms, self.steady_unit) = timed(False, mark=True)
             self.ungated_wall = None
             self.timed_launch = ("hipGraph" if graph is not None else
                                  "eager (long launches: the host enqueues ahead of the GPU)"
