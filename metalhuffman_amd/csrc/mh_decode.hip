@@ -1269,6 +1269,9 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   uint32_t nw = (a.total_tiles + (uint32_t)cus - 1) / (uint32_t)cus;
   if (nw < 1) nw = 1;
   if (nw > (uint32_t)kMaxWavesPerWG) nw = kMaxWavesPerWG;
+#ifdef MH_FORCE_WAVES_PER_WG  // A/B: workgroup width for the config-3 balance study
+  if (a.total_tiles >= (uint32_t)(MH_FORCE_WAVES_PER_WG * cus)) nw = MH_FORCE_WAVES_PER_WG;
+#endif
   a.n_groups = (a.total_tiles + nw - 1) / nw;
 #ifdef MH_GRID_WGS_PER_CU  // A/B: cap the persistent grid below the occupancy limit
   const uint32_t resident = (uint32_t)(cus * min(di->occ[kDelta ? 1 : 0][nw], MH_GRID_WGS_PER_CU));
