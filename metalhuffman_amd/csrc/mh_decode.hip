@@ -182,9 +182,6 @@ struct LdsWords {
   const uint8_t *w;
   __device__ __forceinline__ const uint8_t *at(uint32_t byte_off) const { return w + byte_off; }
 };
-__device__ __forceinline__ uint32_t word_at(const uint8_t *q) {
-  return *reinterpret_cast<const uint32_t *>(q);
-}
 // Stage swizzle (batch kernel, MH_STAGE_SWIZZLE): the eight 16-B chunks of every
 // 128-B row of a wave's stage are permuted by the row index (XOR), so lanes whose
 // blocks start a multiple of 128 B apart -- flat code lengths make every block
@@ -905,15 +902,13 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 // wave, lanes l and l ^ 32 (32 blocks per wave, so twice the waves of the small
 // kernel). Lane A starts at the block's first bit (AAPLShaders.metal:241-268);
 // lane B starts speculatively at the block's middle bit M = off + len/2 (len from
-// the next block's offset) and records which bits in [M, M + 64) start one of its
-// symbols. Huffman paths re-synchronise: once A reaches a bit >= M that B also
-// started a symbol at, the two paths coincide from there on, so A stops and B's
-// symbols from that point are the block's remaining symbols. The cursor hand-off
-// (B's position and start mask to A, A's stop count to B) goes through
-// ds_bpermute. A block whose lanes never meet (or disagree with the block end) is
-// finished serially by lane A. Each lane writes its running output bytes into a
-// per-lane LDS row; the block's rows are assembled from the two (B's bytes rebased
-// by the running delta sum at the meeting point) and stored 8 bytes per row.
+// the next block's offset). Huffman paths re-synchronise: once A reaches a bit >= M
+// at which B also started a symbol, the two paths coincide from there on, so A stops
+// and B's symbols from that point are the block's remaining symbols (lp_decode).
+// Round 3 rewrite: the round-2 kernel exchanged cursors and
+// masks through three ds_bpermutes on every step and stored every symbol to LDS
+// (35.7 vs 5.8 us); this one runs the default step with register output and swaps
+// the window masks only at sparse checkpoints.
 #ifndef MH_LP_WAVES
 #define MH_LP_WAVES 4
 #endif
@@ -925,155 +920,196 @@ __shared__ __attribute__((aligned(16))) uint16_t s_lp_lut[kLut14Entries];
 __shared__ __attribute__((aligned(16))) uint8_t s_lp_stage[kLpWaves * kLpStageBytes];
 __shared__ __attribute__((aligned(16))) uint8_t s_lp_out[kLpWaves * 64 * kLpOutStride];
 
-// Bit cursor over a wave's staged span (byte offsets into the stage).
-template <int kBits>
-struct LpCur {
-  static constexpr uint32_t kCur = 127u - (uint32_t)kBits;
-  static constexpr uint32_t kMask = (2u << kBits) - 2u;
-  static constexpr uint32_t kRefillAt = kCur - 32u;
-  uint32_t hi, lo, nw, wa, wbits, S;
-  __device__ __forceinline__ void init(const uint8_t *stage, uint32_t bit, uint32_t prev) {
-    wa = (bit >> 5) * 4u;
-    wbits = (bit >> 5) * 32u;
-    S = (prev << 8) + kCur - (bit & 31u);
-    hi = word_at(stage + wa);
-    lo = word_at(stage + wa + 4);
-    nw = word_at(stage + wa + 8);
-  }
-  __device__ __forceinline__ uint32_t pos() const { return wbits + kCur - (S & 0xFFu); }
-  // one symbol (the small kernel's step, refilled before every symbol); returns
-  // the output byte: the running delta sum, or the raw symbol
-  template <bool kDelta, bool kEsc>
-  __device__ __forceinline__ uint32_t step(const uint8_t *stage, const uint8_t *lut) {
-    if ((S & 0xFFu) <= kRefillAt) {
-      hi = lo;
-      lo = nw;
-      wa += 4u;
-      wbits += 32u;
-      S += 32u;
-      nw = word_at(stage + wa + 8);
-    }
-    const uint64_t x = (((uint64_t)hi) << 32) | lo;
-    uint32_t e = *reinterpret_cast<const uint16_t *>(lut + ((uint32_t)(x >> (S & 63u)) & kMask));
-    if constexpr (kEsc) {
-      if (e < kEscapeBelow) {
-        const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;
-        e = *reinterpret_cast<const uint16_t *>(lut + 2u * (kL1Entries + ((e & 0xFFu) << kL2Bits) + x3));
-      }
-    }
-    S += e;
-    return kDelta ? ((S >> 8) & 0xFFu) : (((e + 0xFFu) >> 8) & 0xFFu);
-  }
-};
-
 __device__ __forceinline__ uint32_t lane_xchg(uint32_t lane, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ^ 32u) << 2), (int)v);
 }
 
-template <bool kDelta, int kBits, bool kEsc>
-__device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *lut, uint8_t *row_a,
-                                          uint8_t *row_b, uint32_t lane, bool valid, uint32_t p,
-                                          uint32_t mid, uint32_t end, bool exact_end, bool spec,
-                                          uint32_t init, __amdgpu_buffer_rsrc_t out, uint32_t row0,
-                                          uint32_t pitch) {
-  const bool is_b = lane >= 32u;
-  uint8_t *row = is_b ? row_b : row_a;
-  LpCur<kBits> c;
-  c.init(stage, is_b ? mid : p, is_b ? 0u : init);
-  bool act = valid && (!is_b || spec);
-  bool checking = valid && spec;  // A: still looking for the meeting point
-  bool synced = false;
-  uint32_t n = 0, ia = 64, jb = 0, nb_b = 0, end_b = 0, target = 64;
-  uint64_t mask = 0;  // B: symbol starts at mid + k, k < 64
+// bytewise (mod 256) add of c to the four bytes of b
+__device__ __forceinline__ uint32_t add_bytes(uint32_t b, uint32_t c) {
+  const uint32_t c4 = c * 0x01010101u;
+  return ((b & 0x7F7F7F7Fu) + (c4 & 0x7F7F7F7Fu)) ^ ((b ^ c4) & 0x80808080u);
+}
 
-  while (__ballot(act)) {  // wave-uniform
-    const uint32_t pb = c.pos();
-    if (is_b && act && pb - mid < 64u) mask |= 1ull << (pb - mid);
-    const bool need_a = !is_b && act && checking && pb >= mid;
-    const bool need_b = is_b && act && !exact_end;
-    if (__ballot(need_a || need_b)) {
-      // A publishes B's stop count once met; B its cursor (bit 31: finished) and mask
-      const uint32_t w0 = is_b ? (act ? pb : (0x80000000u | end_b)) : (synced ? 0x80000000u | (jb + 64u - ia) : 0u);
-      const uint32_t x0 = lane_xchg(lane, w0);
-      const uint32_t x1 = lane_xchg(lane, (uint32_t)mask);
-      const uint32_t x2 = lane_xchg(lane, (uint32_t)(mask >> 32));
-      if (need_a) {
-        const uint32_t rel = pb - mid;
-        if (rel >= 64u) {
-          checking = false;  // never met within the window: A decodes the whole block
-        } else if ((x0 >> 31) || (x0 & 0x7FFFFFFFu) >= pb) {  // B's mask is final up to pb
-          const uint64_t mb = (((uint64_t)x2) << 32) | x1;
-          if ((mb >> rel) & 1u) {
-            synced = true;
-            checking = false;
+// One block on two lanes (round 3: no per-step exchange).
+//   * Both lanes run the default kernel's step (64-bit window, refill before every
+//     symbol pair, masked next-word read) in one unrolled 64-step loop, so symbol n
+//     goes to a fixed byte of the lane's 16 output registers (v_perm packing).
+//   * Each lane records its own symbol starts in the window [mid, mid + 128) as a
+//     128-bit mask (a 64-bit window leaves 8.4 % of BigBridge's blocks unmatched, this
+//     one 1.4 %; scripts/sim_lane_pairs_ckpt.py). B stops at the block end; A stops at the first start that is also
+//     one of B's, which it tests on every step once it holds B's final mask.
+//   * B's mask reaches A through five ds_bpermutes at sparse checkpoints (every
+//     4 steps from step 8, only while some lane of the wave still waits for it); A
+//     lanes that were already past the meeting point by then stop at the checkpoint
+//     (first common bit of the two masks; their extra symbols are the block's own).
+//   * Afterwards one exchange settles the split: A keeps symbols [0, ia), B supplies
+//     [ia, 64) from its own index jb; if B decoded too few (corrupt input, a partner
+//     that never synchronised) A finishes the block alone. Rows are assembled from the
+//     two lanes' register rows through LDS with dword reads and v_alignbyte; B's
+//     running sums are rebased bytewise by the delta sum at the meeting point.
+template <bool kDelta, class Cfg>
+__device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *lut, uint32_t *row_a,
+                                          uint32_t *row_b, uint32_t lane, bool valid, uint32_t p,
+                                          uint32_t mid, uint32_t end, bool spec, uint32_t init,
+                                          __amdgpu_buffer_rsrc_t out, uint32_t row0, uint32_t pitch) {
+  typedef const __attribute__((address_space(3))) uint8_t *lds_u8;
+  typedef const __attribute__((address_space(3))) uint32_t *lds_u32;
+  const bool is_b = lane >= 32u;
+  const lds_u8 base = (lds_u8)stage;
+  const uint32_t s0 = is_b ? mid : p;
+  lds_u8 wa = base + (s0 >> 5) * 4u;
+  uint32_t wbits = (s0 & ~31u) + Cfg::kCur;  // cursor bit = wbits - (S & 0xFF)
+  uint32_t S = ((is_b ? 0u : init) << 8) + Cfg::kCur - (s0 & 31u);
+  uint32_t kRefill = Cfg::kRefillAt;
+  if constexpr ((Cfg::kRefillAt & 1u) != 0u) asm("s_mov_b32 %0, %1" : "=s"(kRefill) : "n"(Cfg::kRefillAt));
+  uint32_t hi = *(lds_u32)wa, lo = *(lds_u32)(wa + 4), nw = *(lds_u32)(wa + 8);
+  bool act = valid && (!is_b || spec);
+  bool chk = valid && spec && !is_b;  // A: still looking for the meeting point
+  bool have = false;                   // A: holds B's final window mask
+  uint64_t mine0 = 0, mine1 = 0, other0 = 0, other1 = 0;  // starts at mid + [0,64), [64,128)
+  uint32_t nd = 0, srel = 128u;        // symbols decoded; meeting point - mid (128: none)
+  uint32_t o[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) o[k] = 0u;
+
+  const auto step = [&](const int n) {
+    bool c = false;
+    if ((n & 1) == 0) {  // sh < 32 at every pair start (codes <= 16 bits)
+      c = (S & 0xFFu) <= kRefill;
+      hi = c ? lo : hi;
+      lo = c ? nw : lo;
+      const uint32_t d = c ? 4u : 0u;
+      wa += d;
+      wbits += d * 8u;
+      S += d * 8u;
+    }
+    const uint64_t x = (((uint64_t)hi) << 32) | lo;
+    uint32_t e = *(const __attribute__((address_space(3))) uint16_t *)(
+        (lds_u8)lut + ((uint32_t)(x >> (S & 63u)) & Cfg::kMask));
+    if ((n & 1) == 0 && c) nw = *(lds_u32)(wa + 8);
+    if constexpr (Cfg::kEsc) {
+      const bool esc = e < kEscapeBelow;
+      if (__builtin_expect(__ballot(esc) != 0, 0)) {
+        const uint32_t x3 = (uint32_t)(x >> ((S - 2u) & 63u)) & 7u;
+        const uint32_t e2 = *(const __attribute__((address_space(3))) uint16_t *)(
+            (lds_u8)lut + 2u * (kL1Entries + ((e & 0xFFu) << kL2Bits) + x3));
+        e = esc ? e2 : e;
+      }
+    }
+    S += e;
+    o[n >> 2] = __builtin_amdgcn_perm(kDelta ? S : e + 0xFFu, o[n >> 2], ins_sel1(n & 3));
+  };
+
+#pragma unroll
+  for (int n = 0; n < 64; ++n) {
+    if ((n & 1) == 0 && !__ballot(act)) break;  // wave-uniform
+    if (n >= 8 && (n & 3) == 0) {
+      const bool need = chk && !have;
+      if (__ballot(need)) {
+        const uint32_t pos = wbits - (S & 0xFFu);
+        const bool fin = !act || (int)(pos - mid) >= 128;  // B: its window mask is final
+        const uint32_t xf = lane_xchg(lane, fin ? 1u : 0u);
+        const uint32_t x0 = lane_xchg(lane, (uint32_t)mine0);
+        const uint32_t x1 = lane_xchg(lane, (uint32_t)(mine0 >> 32));
+        const uint32_t x2 = lane_xchg(lane, (uint32_t)mine1);
+        const uint32_t x3 = lane_xchg(lane, (uint32_t)(mine1 >> 32));
+        if (need && xf) {
+          have = true;
+          other0 = ((uint64_t)x1 << 32) | x0;
+          other1 = ((uint64_t)x3 << 32) | x2;
+          const uint64_t c0 = mine0 & other0, c1 = mine1 & other1;
+          if (c0 | c1) {  // already past the meeting point
+            chk = false;
             act = false;
-            ia = n;
-            jb = (uint32_t)__builtin_popcountll(mb & ((1ull << rel) - 1u));
+            srel = c0 ? (uint32_t)__builtin_ctzll(c0) : 64u + (uint32_t)__builtin_ctzll(c1);
+          } else if ((int)(pos - mid) >= 128) {
+            chk = false;  // passed the window without meeting: A decodes the block alone
           }
         }
       }
-      if (need_b && (x0 >> 31)) target = x0 & 0x7Fu;
     }
     if (act) {
-      row[n] = (uint8_t)c.template step<kDelta, kEsc>(stage, lut);
-      ++n;
-      if (is_b) {
-        const uint32_t pa = c.pos();
-        if ((exact_end && pa >= end) || n >= target || n >= 64u) {
+      const uint32_t rel = (wbits - (S & 0xFFu)) - mid;
+      if (rel < 128u) {
+        const uint64_t bit = 1ull << (rel & 63u);
+        const bool w1 = rel >= 64u;
+        if (chk && have && ((w1 ? other1 : other0) & bit)) {
+          chk = false;
           act = false;
-          nb_b = n;
-          end_b = pa;
+          srel = rel;
+        } else if (w1) {
+          mine1 |= bit;
+        } else {
+          mine0 |= bit;
         }
-      } else if (n >= 64u) {
-        act = false;
+      } else if (chk && have && (int)rel >= 128) {
+        chk = false;
       }
+    }
+    if (act) {
+      step(n);
+      nd = (uint32_t)n + 1u;
+      if ((is_b && (wbits - (S & 0xFFu)) >= end) || n == 63) act = false;
     }
   }
-  // Meeting point consistent with B's end? (B must reach the block end exactly
-  // after jb + 64 - ia symbols.) Otherwise A finishes the block from where it stopped.
-  {
-    const uint32_t wa = synced ? (0x80000000u | (ia << 8) | jb) : 0u;
-    const uint32_t wb = nb_b | ((!exact_end || end_b == end) ? 0x80000000u : 0u);
-    const uint32_t x = lane_xchg(lane, is_b ? wb : wa);
-    bool repair = false;
-    if (!is_b && synced) {
-      const bool ok = (x >> 31) && (x & 0x7Fu) == jb + 64u - ia;
-      if (!ok) {
-        synced = false;
-        repair = true;
-      }
-    }
-    while (__ballot(repair)) {
-      if (repair) {
-        row[n] = (uint8_t)c.template step<kDelta, kEsc>(stage, lut);
-        if (++n >= 64u) repair = false;
-      }
-    }
+
+  // the split: A's symbols before the meeting point (ia), B's (jb)
+  const bool met = !is_b && srel < 128u;
+  uint32_t ia = 64u, jb = 0u;
+  if (met) {  // A's starts at or after the meeting point; B's before it
+    const bool lo = srel < 64u;
+    const uint32_t r = srel & 63u;
+    ia = nd - (lo ? (uint32_t)__builtin_popcountll(mine0 >> r) + (uint32_t)__builtin_popcountll(mine1)
+                  : (uint32_t)__builtin_popcountll(mine1 >> r));
+    jb = lo ? (uint32_t)__builtin_popcountll(other0 & ((1ull << r) - 1ull))
+            : (uint32_t)__builtin_popcountll(other0) + (uint32_t)__builtin_popcountll(other1 & ((1ull << r) - 1ull));
   }
-  // Assemble and store: lane A rows 0-3, lane B rows 4-7 of the block.
-  const uint32_t fin = lane_xchg(lane, synced ? (0x80000000u | (ia << 8) | jb) : 0u);
-  const uint32_t f = is_b ? fin : (synced ? (0x80000000u | (ia << 8) | jb) : 0u);
+  const uint32_t nb_b = lane_xchg(lane, nd);
+  const bool ok = met && nb_b >= jb + 64u - ia;
+  // B decoded too few symbols past the meeting point: A finishes the block alone
+  const bool rep = met && !ok;
+  if (__ballot(rep)) {
+#pragma unroll
+    for (int n = 0; n < 64; ++n)
+      if (rep && (uint32_t)n >= nd) step(n);
+  }
+  const uint32_t dec = ok ? (0x80000000u | (ia << 8) | jb) : 0u;
+  const uint32_t decx = lane_xchg(lane, dec);
+  const uint32_t f = is_b ? decx : dec;
   const bool split = (f >> 31) != 0;
-  const uint32_t i_a = split ? (f >> 8) & 0x7Fu : 64u;
-  const uint32_t j_b = f & 0x7Fu;
-  wave_sync();  // every lane's row bytes -> reads
-  const uint32_t pa = i_a ? row_a[i_a - 1u] : init;
-  const uint32_t lb = j_b ? row_b[j_b - 1u] : 0u;
-  const uint32_t cadd = kDelta ? ((pa - lb) & 0xFFu) : 0u;
+  ia = split ? (f >> 8) & 0x7Fu : 64u;
+  jb = f & 0x7Fu;
+
+  uint32_t *row = is_b ? row_b : row_a;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) row[k] = o[k];
+  wave_sync();  // both lanes' rows -> reads
+  uint32_t cadd = 0;
+  if (kDelta) {
+    const uint32_t pa = ia ? reinterpret_cast<const uint8_t *>(row_a)[ia - 1u] : init;
+    const uint32_t pb = jb ? reinterpret_cast<const uint8_t *>(row_b)[jb - 1u] : 0u;
+    cadd = (pa - pb) & 0xFFu;
+  }
   const uint32_t r0 = is_b ? 4u : 0u;
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
-    uint32_t w[2] = {0u, 0u};
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint32_t i = (r0 + r) * 8u + k;
-      const uint32_t v = i < i_a ? row_a[i] : ((row_b[i - i_a + j_b] + cadd) & 0xFFu);
-      w[k >> 2] |= v << (8u * (k & 3u));
-    }
-    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
     v2u32 v;
-    v.x = w[0];
-    v.y = w[1];
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint32_t q = (r0 + r) * 2u + h;
+      const uint32_t aw = row_a[q];
+      // B byte index of output byte 4q, + 8 (>= 5 whenever a byte of this word is B's;
+      // the clamp only keeps all-A words' unused reads inside the LDS rows)
+      int u = (int)(4u * q + 8u + jb) - (int)ia;
+      u = u < 4 ? 4 : u;
+      uint32_t bw = __builtin_amdgcn_alignbyte(row_b[(u >> 2) - 1], row_b[(u >> 2) - 2], (uint32_t)u & 3u);
+      if (kDelta) bw = add_bytes(bw, cadd);
+      const int na = (int)ia - (int)(4u * q);  // leading bytes of this word from A
+      const uint32_t m = na >= 4 ? 0xFFFFFFFFu : na <= 0 ? 0u : (1u << (8 * na)) - 1u;
+      const uint32_t w = (aw & m) | (bw & ~m);
+      if (h == 0) v.x = w; else v.y = w;
+    }
     const uint32_t off = valid ? row0 + (r0 + r) * pitch : 0xFFFFFFF0u;
     __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
   }
@@ -1085,8 +1121,8 @@ __global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const
   const uint32_t bl = lane & 31u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t *stage = s_lp_stage + wave * kLpStageBytes;
-  uint8_t *row_a = s_lp_out + (wave * 64u + bl) * kLpOutStride;
-  uint8_t *row_b = row_a + 32u * kLpOutStride;
+  uint32_t *row_a = reinterpret_cast<uint32_t *>(s_lp_out + (wave * 64u + bl) * kLpOutStride);
+  uint32_t *row_b = reinterpret_cast<uint32_t *>(s_lp_out + (wave * 64u + 32u + bl) * kLpOutStride);
   const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lp_lut);
   const uint8_t *prepared = reinterpret_cast<const uint8_t *>(a.lut);
   const uint32_t max_len = *reinterpret_cast<const uint32_t *>(prepared + kMaxLenOff);
@@ -1169,13 +1205,14 @@ __global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const
   const uint32_t len = end_l - off;
   const uint32_t mid = t.p + (len >> 1);
   const uint32_t end = t.p + len;
-  const bool spec = t.valid && len >= 2u * (uint32_t)MH_LP_MIN_BITS && len <= 64u * 16u;
+  // the frame's last block has no exact end: lane A alone
+  const bool spec = t.valid && exact_end && len >= 2u * (uint32_t)MH_LP_MIN_BITS && len <= 64u * 16u;
   if (l14)
-    lp_decode<kDelta, kLut14Bits, false>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end, exact_end,
-                                         spec, init, out, row0, (uint32_t)a.out_pitch);
+    lp_decode<kDelta, StepCfg<kLut14Bits, false>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
+                                                  spec, init, out, row0, (uint32_t)a.out_pitch);
   else
-    lp_decode<kDelta, kLutBits, true>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end, exact_end,
-                                      spec, init, out, row0, (uint32_t)a.out_pitch);
+    lp_decode<kDelta, StepCfg<kLutBits, false>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
+                                                spec, init, out, row0, (uint32_t)a.out_pitch);
 }
 
 // Per-device launch parameters (CU count, batch-kernel occupancy per workgroup
