@@ -986,7 +986,7 @@ __device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *l
     const uint64_t x = (((uint64_t)hi) << 32) | lo;
     uint32_t e = *(const __attribute__((address_space(3))) uint16_t *)(
         (lds_u8)lut + ((uint32_t)(x >> (S & 63u)) & Cfg::kMask));
-    if ((n & 1) == 0 && c) nw = *(lds_u32)(wa + 8);
+    if ((n & 1) == 0) nw = *(lds_u32)(wa + 8);
     if constexpr (Cfg::kEsc) {
       const bool esc = e < kEscapeBelow;
       if (__builtin_expect(__ballot(esc) != 0, 0)) {
@@ -1028,28 +1028,25 @@ __device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *l
         }
       }
     }
-    if (act) {
+    {
+      // window bookkeeping, branch-free (selects, no exec-mask branches)
       const uint32_t rel = (wbits - (S & 0xFFu)) - mid;
-      if (rel < 128u) {
-        const uint64_t bit = 1ull << (rel & 63u);
-        const bool w1 = rel >= 64u;
-        if (chk && have && ((w1 ? other1 : other0) & bit)) {
-          chk = false;
-          act = false;
-          srel = rel;
-        } else if (w1) {
-          mine1 |= bit;
-        } else {
-          mine0 |= bit;
-        }
-      } else if (chk && have && (int)rel >= 128) {
-        chk = false;
-      }
+      const bool inw = act && rel < 128u;
+      const uint64_t bit = 1ull << (rel & 63u);
+      const uint64_t b0 = (inw && rel < 64u) ? bit : 0ull;
+      const uint64_t b1 = (inw && rel >= 64u) ? bit : 0ull;
+      const bool look = chk && have;
+      const bool hit = look && ((other0 & b0) | (other1 & b1)) != 0ull;
+      srel = hit ? rel : srel;
+      chk = chk && !hit && !(look && act && !inw && (int)rel >= 128);
+      act = act && !hit;
+      mine0 |= hit ? 0ull : b0;
+      mine1 |= hit ? 0ull : b1;
     }
     if (act) {
       step(n);
       nd = (uint32_t)n + 1u;
-      if ((is_b && (wbits - (S & 0xFFu)) >= end) || n == 63) act = false;
+      act = !((is_b && (wbits - (S & 0xFFu)) >= end) || n == 63);
     }
   }
 

@@ -45,7 +45,7 @@ def path(start, steps=64):
     return P
 
 
-WIN = int(os.environ.get("WIN", "64"))  # window bits
+WIN = int(os.environ.get("WIN", "128"))  # window bits (the kernel: 128)
 A = path(offs)            # A's starts: A[:, k] = start of symbol k (true path)
 B = path(mid)             # B's starts from the middle
 stepsA = np.full(nb, 64)
@@ -97,3 +97,4 @@ print(f"wave loop length (32 blocks): p50 {np.median(wm):.0f} p90 {np.percentile
       f"p99 {np.percentile(wm, 99):.0f} max {wm.max()}  (default kernel: 64 on every wave)")
 print(f"lane-steps per block: {(stepsA + stepsB).mean():.1f} (default 64)")
 print(f"blocks where A decodes all 64: {(stepsA == 64).mean() * 100:.2f} %")
+print(f"wave loop length mean {wm.mean():.1f} over {wm.size} waves")

@@ -52,3 +52,20 @@ def long_span_deltas(width: int, height: int, seed: int = 0) -> np.ndarray:
     rare = r.integers(1, 256, size=first, dtype=np.uint8)
     d[:first] = rare
     return d
+
+
+def lane_pair_oversize_deltas(seed: int = 0) -> np.ndarray:
+    """512x512 deltas whose first 32 blocks hold 249 rare symbols x 8 (15-bit codes under
+    a geometric chain of 7 common symbols): that 32-block lane-pair tile spans 3,735 B,
+    more than round 2's 3,712-B lane-pair stage, with codes above 14 bits
+    (the 13-bit table with escapes)."""
+    n = 512 * 512
+    r = np.random.default_rng(seed)
+    rare = np.repeat(np.arange(7, 256, dtype=np.uint8), 8)
+    head = np.zeros(2048, np.uint8)
+    head[: rare.size] = rare
+    r.shuffle(head)
+    rest = np.repeat(np.arange(7, dtype=np.uint8), [n >> (k + 1) for k in range(7)])[: n - 2048]
+    rest = np.concatenate([rest, np.zeros(n - 2048 - rest.size, np.uint8)])
+    r.shuffle(rest)
+    return np.concatenate([head, rest])

@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from helpers import fibonacci_deltas, image_from_block_deltas
+from helpers import fibonacci_deltas, image_from_block_deltas, lane_pair_oversize_deltas
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +70,17 @@ def test_long_codes_escape_table(mh, oracle, device, n_sym):
     d = fibonacci_deltas(n_sym, 512 * 512, seed=n_sym)
     img = image_from_block_deltas(d, 512, 512)
     ef = mh.encode_frame(img)
+    out = _decode([ef], device)[0]
+    assert np.array_equal(out, img)
+    assert np.array_equal(out, _oracle(oracle, ef))
+
+
+def test_largest_lane_pair_span(mh, oracle, device):
+    """A 32-block tile of 15-bit codes (3,735 B of code bytes) fits the lane-pair stage."""
+    img = image_from_block_deltas(lane_pair_oversize_deltas(), 512, 512)
+    ef = mh.encode_frame(img)
+    o = ef.block_offsets.astype(np.int64)
+    assert ef.canon.max() == 15 and (o[32] - o[0]) / 8 > 3712
     out = _decode([ef], device)[0]
     assert np.array_equal(out, img)
     assert np.array_equal(out, _oracle(oracle, ef))
