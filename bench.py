@@ -178,22 +178,29 @@ class Workload:
         torch.cuda.synchronize(dev)
         # Long launches (>= LONG_LAUNCH_PIXELS decoded per launch: the 64-frame batch, the
         # 8192^2 frame; 20-70 us each) replay a graph of LONG_GRAPH_LAUNCHES launches
-        # K / LONG_GRAPH_LAUNCHES times behind the launch gate: one graph of all K queued
-        # behind the gate ran 13-17 % slower per dispatch under rocprofv3 than the same
-        # launches unprofiled (profiles/r03_gate_rocprof_artifact.txt), and plain eager
-        # regions dispatch 5-8 % slower than queued ones (profiles/r03_long_launch_ab.txt).
-        # A launch of >= 113 MB leaves nothing warm in the 256 MiB Infinity Cache for the
-        # next replay of the same sequence. Short launches (one 2048x1536 frame, ~5.5 us)
-        # keep one graph of the K distinct launches (or eager launches behind the gate).
-        # Decided by size, not by a timing probe: under a profiler the probe itself slows.
+        # K / LONG_GRAPH_LAUNCHES times; the first replay is queued behind the launch gate,
+        # the rest are enqueued once it opens (the host runs ~1 ms ahead of the GPU).
+        # Queuing every replay behind the gate times the same unprofiled (66.9-67.0 vs
+        # 66.9-67.6 us per batch launch) but ran 15-20 % slower per dispatch under
+        # rocprofv3 (78.3 vs 68.3 us batch, 30.4 vs 25.3 us 8192^2), which made the profile
+        # disagree with the line (profiles/r03_window_ab.txt, r03_gate_rocprof_artifact.txt);
+        # plain eager regions dispatch 5-8 % slower than queued ones
+        # (profiles/r03_long_launch_ab.txt). A launch of >= 113 MB leaves nothing warm in
+        # the 256 MiB Infinity Cache for the next replay of the same sequence. Short
+        # launches (one 2048x1536 frame, ~5.5 us) keep one graph of the K distinct launches
+        # (or eager launches behind the gate). Decided by size, not by a timing probe:
+        # under a profiler the probe itself slows.
+        # MH_BENCH_LONG (A/B): window (default) | graph (every replay behind the gate) |
+        # graph_ungated | eager
         self.long_launches = self.pixels >= LONG_LAUNCH_PIXELS
-        mode = os.environ.get("MH_BENCH_LONG", "graph")
+        mode = os.environ.get("MH_BENCH_LONG", "window")
         if self.long_launches and mode == "eager":
             use_graph = gate = False
         if self.long_launches and mode == "graph_ungated":  # A/B: the same replays, no gate
             gate = False
+        window = self.long_launches and mode == "window"
         G = steps  # launches per captured graph
-        if self.long_launches and mode.startswith("graph") and steps % LONG_GRAPH_LAUNCHES == 0:
+        if self.long_launches and mode in ("window", "graph", "graph_ungated") and steps % LONG_GRAPH_LAUNCHES == 0:
             G = LONG_GRAPH_LAUNCHES
         self.graph_launches = G
         graph = None
@@ -264,11 +271,15 @@ class Workload:
             torch.cuda.synchronize(dev)
             if gated:
                 GATE.arm(torch.cuda.current_stream(dev).cuda_stream)
+            nrep = steps // G
+            # replays queued behind the gate (window mode: the first only, the rest are
+            # enqueued once the gate is open, the host running ahead of the GPU)
+            pre = nrep if not (gated and window) else min(1, nrep)
             if gated or graph is not None:
                 if events:
                     r0.record()
                 if graph is not None and not (gated and eager_gated):
-                    for r in range(steps // G):
+                    for r in range(pre):
                         graph.replay()
                         if r == 0 and events:
                             rA.record()
@@ -280,13 +291,18 @@ class Workload:
                         self.launch(i, relaxed=relax and i > 0)
                         if i == 0 and events:
                             rA.record()
-                if events:
+                if events and pre == nrep:
                     r1.record()
             # (no barrier while a gate is armed: an RCCL barrier would queue behind it;
             # each rank times its own region, the max over ranks is taken below)
             t0 = time.perf_counter()
             if gated:
                 GATE.open()
+                if pre < nrep:
+                    for r in range(pre, nrep):
+                        graph.replay()
+                    if events:
+                        r1.record()
             else:
                 r0.record()
                 if graph is not None:
@@ -334,7 +350,9 @@ class Workload:
             self.ungated_wall, _, _ = timed(False)
             self.timed_launch = (("eager behind the launch gate" + (", launches 2..K with MH_FLAG_ANY_ORDER" if ANY_ORDER else ""))
                                  if eager_gated else
-                                 f"{steps // G} replays of a {G}-launch hipGraph behind the launch gate")
+                                 (f"{steps // G} replays of a {G}-launch hipGraph, the first behind the launch gate, "
+                                  "the rest enqueued once it opens" if window else
+                                  f"{steps // G} replays of a {G}-launch hipGraph behind the launch gate"))
         else:
             wall, region_ms, (steady_ms, self.steady_unit) = timed(False, mark=True)
             self.ungated_wall = None
