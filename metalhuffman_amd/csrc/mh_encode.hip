@@ -425,6 +425,9 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   __shared__ unsigned long long s_total;
   const uint32_t tid = threadIdx.x;
   const bool sym_thread = tid < 256u;  // thread tid < 256 owns symbol tid
+  // this call's table tag: meta[kGen] does not change during the launch, so its L2
+  // round trip overlaps the histogram loads instead of preceding the publication
+  const uint32_t tag = kFused && sym_thread ? table_tag(meta) : 0u;
   uint64_t f = 0;
   if (sym_thread) {
 #pragma unroll
@@ -702,17 +705,34 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   }
   if constexpr (!kFused) table[tid] = e;
   __shared__ uint32_t s_bad2;
-  uint32_t published = 0;
+  __shared__ unsigned long long s_len_bytes;
   if (tid == 0) {
     const uint64_t total = s_total;
     const uint64_t len = (total + 7) / 8 + MH_CODES_PAD;  // + encoder's 2 and renderer's 2 zero bytes
     uint32_t bad = s_bad;
     if (!bad && (total >= (1ull << 32) || ((len + 3) & ~3ull) > codes_cap)) bad = (uint32_t)-MH_ERR_CAPACITY;
     s_bad2 = bad;
+    s_len_bytes = len;
+  }
+  if constexpr (kFused) {
+    // Publication first (the packing workgroups wait on it; nothing they read comes
+    // from the bookkeeping below): each table word carries this call's tag (bits 8-15)
+    // and, for a rejected frame, the bad bit (7): a packing workgroup polls the words
+    // themselves, each valid on its own -- one relaxed agent-scope atomic per word, no
+    // flag to order against the table (no release/acquire pair, no vmcnt reliance) and
+    // no second round trip for the table after the flag.
+    __syncthreads();
+    __hip_atomic_store(&table[tid], e | (tag << 8) | (s_bad2 ? 0x80u : 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    MH_CODE_STAMP(0, 1)
+  }
+  if (tid == 0) {
+    const uint32_t bad = s_bad2;
+    const uint64_t len = s_len_bytes;
     meta[0] = bad ? 0 : len;
     meta[1] = bad ? 0 : 1;
     meta[kTicket] = 0;
-    meta[kTotalBits] = total;
+    meta[kTotalBits] = s_total;
     if (codes_len_out) *codes_len_out = bad ? 0 : len;
     if (status) {
       if constexpr (kFused) {
@@ -727,21 +747,7 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
         *status = bad ? -(int32_t)bad : MH_OK;
       }
     }
-    published = bad ? 2u : 1u;
   }
-  if constexpr (kFused) {
-    // Publication: each table word carries this call's tag (bits 8-15) and, for a
-    // rejected frame, the bad bit (7): a packing workgroup polls the words themselves,
-    // each valid on its own -- one relaxed agent-scope atomic per word, no flag to order
-    // against the table (no release/acquire pair, no vmcnt reliance) and no second
-    // round trip for the table after the flag.
-    __syncthreads();
-    const uint32_t tag = table_tag(meta);
-    __hip_atomic_store(&table[tid], e | (tag << 8) | (s_bad2 ? 0x80u : 0u), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    MH_CODE_STAMP(0, 1)
-  }
-  (void)published;
   MH_TREE_STAMP(8);
 }
 
