@@ -36,7 +36,7 @@ namespace {
 #ifndef MH_MAX_WAVES
 #define MH_MAX_WAVES 8
 #endif
-#ifndef MH_DIAG_BROADCAST_LUT   // diagnostic builds only: LUT index forced to 0 (wrong output)
+#ifndef MH_DIAG_BROADCAST_LUT   // diagnostic builds only: every lane reads LUT entry 0 (wrong output)
 #define MH_DIAG_BROADCAST_LUT 0
 #endif
 #ifndef MH_MIN_WAVES_PER_EU     // register cap: 6 waves/SIMD = what the LDS budget admits
@@ -292,10 +292,16 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   uint32_t lo = rd(wa + 4);
   uint32_t nw = rd(wa + 8);
   (void)prio;
+  // MH_DIAG_BROADCAST_LUT: every lookup address ANDed with an opaque zero, so the read
+  // stays on the chain (a literal 0 let the compiler hoist it out of the loop) but every
+  // lane reads entry 0: conflict-free broadcasts, wrong output (diagnostic builds only)
+  uint32_t diag_zero = 0;
+  if constexpr (MH_DIAG_BROADCAST_LUT != 0) asm volatile("v_mov_b32 %0, 0" : "=v"(diag_zero));
+  (void)diag_zero;
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_LOOKUP(A1)                                                               \
-  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? 0u : (A1)));
+  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? (A1) & diag_zero : (A1)));
 #define MH_FINISH(J, OW)                                                            \
   {                                                                                 \
     if constexpr (Cfg::kEsc) {                                                      \
