@@ -48,6 +48,12 @@ namespace {
 #ifndef MH_NT_STORE
 #define MH_NT_STORE 1
 #endif
+#ifndef MH_STORE_AUX            // batch kernel row-store cache bits (gfx950 aux: 1 sc0, 2 nt, 16 sc1)
+#define MH_STORE_AUX (MH_NT_STORE ? 2 : 0)
+#endif
+#ifndef MH_SMALL_STORE_AUX      // small-launch kernel: nt sc1, write-through (nothing dirty is left
+#define MH_SMALL_STORE_AUX 18   //    in the XCDs' L2s for the end-of-kernel release to write back)
+#endif
 #ifndef MH_SPEC_REFILL          // 1: refill folded into the pair's first lookup (A/B)
 #define MH_SPEC_REFILL 0
 #endif
@@ -233,8 +239,9 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 //   window the refill selects (two shifts in parallel), taking the word move off
 //   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
 template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits,
-          bool kSwizzle = false>
+          bool kSwizzle = false, int kStoreAux = MH_STORE_AUX>
 struct StepCfg {
+  static constexpr int kAux = kStoreAux;  // row-store cache bits
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
   static constexpr bool kSpec = kSpecRefill;
@@ -399,7 +406,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
       v.x = o0;
       v.y = o1;
       const uint32_t off = rbase + r * pitch;
-      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
+      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, Cfg::kAux);
     }
   }
 #undef MH_STEP
@@ -871,21 +878,24 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   const OutTile ot = out_tile(a, t, lane);
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
   const uint32_t row0 = ot.row0;
+  // the small kernel's step flavours (all with write-through row stores)
+  using Small14 = StepCfg<kLut14Bits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0, false, false, MH_SMALL_STORE_AUX>;
+  using Small13 = StepCfg<kLutBits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0, true, false, MH_SMALL_STORE_AUX>;
+  using Halves14 = StepCfg<kLut14Bits, true, false, false, false, MH_SMALL_STORE_AUX>;
+  using Halves13 = StepCfg<kLutBits, true, false, true, false, MH_SMALL_STORE_AUX>;
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
     MH_STAMP(3);
     LdsWords src{stage};
     if (l14)
-      decode_block<kDelta, StepCfg<kLut14Bits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0>>(src, lut, t.p, t.init, out, row0,
-                                                      (uint32_t)a.out_pitch, !t.valid);
+      decode_block<kDelta, Small14>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
     else
-      decode_block<kDelta, StepCfg<kLutBits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0>>(src, lut, t.p, t.init, out, row0,
-                                                    (uint32_t)a.out_pitch, !t.valid);
+      decode_block<kDelta, Small13>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
   } else if (l14) {
-    decode_halves<kDelta, StepCfg<kLut14Bits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
+    decode_halves<kDelta, Halves14>(a, t, lane, lut, stage, out, row0, !t.valid);
   } else {
-    decode_halves<kDelta, StepCfg<kLutBits, true>>(a, t, lane, lut, stage, out, row0, !t.valid);
+    decode_halves<kDelta, Halves13>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
 #if MH_TLB_PREFETCH
   if (warm == 0x9E3779B9u && lane == 64u) a.out[0] = 0;  // never true (lane < 64): keeps the loads
@@ -1114,7 +1124,7 @@ __device__ __forceinline__ void lp_decode(const uint8_t *stage, const uint8_t *l
       if (h == 0) v.x = w; else v.y = w;
     }
     const uint32_t off = valid ? row0 + (r0 + r) * pitch : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, MH_NT_STORE ? 2 : 0);
+    __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, Cfg::kAux);
   }
 }
 

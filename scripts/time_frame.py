@@ -24,6 +24,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=16)
 ap.add_argument("--k", type=int, default=200)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--batch", type=int, default=1, help="frames per launch (64: the config-4 shard)")
 ap.add_argument("--tag", default=os.path.basename(os.environ.get("MH_LIB", "default")))
 args = ap.parse_args()
 
@@ -32,7 +33,10 @@ bb = F.bigbridge()
 efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.frames)]
 t1, t2 = efs[0].tables()
 tabs = D.DeviceTables.upload(t1, t2, "cuda")
-frs = [D.DeviceFrames.pack([e], "cuda") for e in efs]
+if args.batch > 1:
+    frs = [D.DeviceFrames.pack([efs[(j + i) % len(efs)] for i in range(args.batch)], "cuda") for j in range(2)]
+else:
+    frs = [D.DeviceFrames.pack([e], "cuda") for e in efs]
 outs = [D.decode(f, tabs) for f in frs]
 for i in range(64):
     D.decode(frs[i % len(frs)], tabs, outs[i % len(frs)])
