@@ -409,3 +409,35 @@ def test_any_order_run_of_frames(mh, oracle, device, bigbridge, lane_pairs):
     bad = [i for i in range(1, len(efs) - 1) if not torch.equal(outs[i][0], ref[i])]
     assert not bad, bad
     assert np.array_equal(outs[3][0].cpu().numpy(), _oracle_decode(oracle, efs[3]))
+
+
+def test_cached_frame_struct_follows_buffers(mh, device, bigbridge):
+    """decoder.decode keeps the mh_frame struct on the DeviceFrames (the per-call Python
+    cost is what an eager caller pays per frame): swapping a buffer tensor, the tables or
+    the extra flags must give a fresh struct, and a too-small / wrong-device `out` is refused
+    before anything launches."""
+    import torch
+    from metalhuffman_amd import _native as N, decoder as D, frames as F
+    a = mh.encode_frame(bigbridge)
+    b = mh.encode_frame(F.block_shuffle(bigbridge, 3))
+    t1, t2 = a.tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    fa, fb = D.DeviceFrames.pack([a], device), D.DeviceFrames.pack([b], device)
+    out = D.decode(fa, tabs)
+    assert np.array_equal(out[0, :, :2048].cpu().numpy(), bigbridge)
+    s0 = D._frame_struct(fa, tabs)
+    assert D._frame_struct(fa, tabs) is s0  # reused while nothing changed
+    assert D._frame_struct(fa, tabs, N.MH_FLAG_ANY_ORDER).flags == s0.flags | N.MH_FLAG_ANY_ORDER
+    # re-seat frame a's buffers with frame b's: the cache must follow
+    fa.codes, fa.block_offsets = fb.codes, fb.block_offsets
+    D.decode(fa, tabs, out, extra_flags=N.MH_FLAG_ANY_ORDER)
+    torch.cuda.synchronize(device)
+    assert np.array_equal(out[0, :, :2048].cpu().numpy(), F.block_shuffle(bigbridge, 3))
+    assert D._frame_struct(fa, tabs).d_codes == fb.codes.data_ptr()
+    # new tables object (same contents): new struct pointing at its buffers
+    tabs2 = D.DeviceTables.upload(t1, t2, device)
+    assert D._frame_struct(fa, tabs2).d_lut == tabs2.lut.data_ptr()
+    with pytest.raises(ValueError):
+        D.decode(D.DeviceFrames.pack([a, b], device), tabs, out)  # room for 1 frame, not 2
+    with pytest.raises(ValueError):
+        D.decode(fa, tabs, torch.empty_like(out, device="cpu"))
