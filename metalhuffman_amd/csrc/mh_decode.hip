@@ -51,6 +51,9 @@ namespace {
 #ifndef MH_STORE_AUX            // batch kernel row-store cache bits (gfx950 aux: 1 sc0, 2 nt, 16 sc1)
 #define MH_STORE_AUX (MH_NT_STORE ? 2 : 0)
 #endif
+#ifndef MH_REFILL_PIN           // 1: pin the masked refill's hi/lo selects before the read
+#define MH_REFILL_PIN 1
+#endif
 #ifndef MH_SMALL_STORE_AUX      // small-launch kernel: nt sc1, write-through (nothing dirty is left
 #define MH_SMALL_STORE_AUX 18   //    in the XCDs' L2s for the end-of-kernel release to write back)
 #endif
@@ -344,6 +347,10 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     /* swizzled stage: keep wa one register (else it is re-derived as a sum of */  \
     /* every step's d inside each masked refill, which spills)                */  \
     if constexpr (Cfg::kSwz) asm volatile("" : "+v"(wa));                          \
+    /* masked refill: the selects stay selects (v_cndmask) -- else the compiler   */  \
+    /* folds them into the masked read's if-block as exec-masked copies (8 moves  */  \
+    /* at every row start)                                                        */  \
+    if constexpr (Cfg::kMasked && MH_REFILL_PIN) asm volatile("" : "+v"(hi), "+v"(lo)); \
     S += d * 8u;                                                                    \
     if constexpr (!Cfg::kMasked) nw = rd(wa + 8);                                   \
   }
