@@ -88,6 +88,44 @@ inline void decode_block(const uint16_t *flat, const uint8_t *codes, uint64_t n,
   }
 }
 
+// kGroup neighbouring blocks of one block row decoded in lock-step: each block's
+// 64-step chain (cursor -> window load -> table load -> cursor) is latency-bound on
+// its own, so the blocks' independent chains are interleaved for the core to overlap.
+// Same per-block semantics as decode_block's fast path; the caller checks that every
+// block of the group takes that path. Writes the group's 8 x (8 * kGroup) pixels to
+// `tile` (row pitch 8 * kGroup).
+constexpr int kGroup = 8;
+inline bool group_fast(const uint32_t *roots, uint64_t n) {
+  uint32_t mx = 0;
+  for (int g = 0; g < kGroup; ++g) mx = std::max(mx, roots[g]);
+  return ((uint64_t)mx >> 3) + 8 + 136 <= n;
+}
+inline void decode_group(const uint16_t *flat, const uint8_t *codes, const uint32_t *roots,
+                         const uint8_t *inits, bool delta, uint8_t *tile) {
+  const uint8_t *p[kGroup];
+  uint64_t pos[kGroup];
+  uint8_t prev[kGroup];
+  for (int g = 0; g < kGroup; ++g) {
+    p[g] = codes + (roots[g] >> 3);
+    pos[g] = roots[g] & 7u;
+    prev[g] = inits ? inits[g] : 0;
+  }
+  for (int r = 0; r < 8; ++r)
+    for (int c = 0; c < 8; ++c) {
+#pragma GCC unroll 8
+      for (int g = 0; g < kGroup; ++g) {
+        uint64_t w;
+        std::memcpy(&w, p[g] + (pos[g] >> 3), 8);
+        w = __builtin_bswap64(w) << (pos[g] & 7);
+        const uint16_t e = flat[w >> 48];
+        pos[g] += e >> 8;
+        const uint8_t sym = (uint8_t)e;
+        prev[g] = (uint8_t)(prev[g] + sym);
+        tile[r * (8 * kGroup) + g * 8 + c] = delta ? prev[g] : sym;
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -144,9 +182,19 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
   flatten(table1, table2, table2_entries, flat.data());
   const auto rows = [&](uint32_t by0, uint32_t by1) {
     uint8_t blk[64];
+    alignas(64) uint8_t tile[8 * 8 * kGroup];
+    const uint32_t gw = width / (8 * kGroup);  // whole groups of full-width blocks per block row
     for (uint32_t by = by0; by < by1; ++by)
       for (uint32_t bx = 0; bx < bw; ++bx) {
         const uint32_t b = by * bw + bx;
+        if (bx % kGroup == 0 && bx / kGroup < gw && group_fast(block_offsets + b, codes_bytes)) {
+          decode_group(flat.data(), codes, block_offsets + b, block_init ? block_init + b : nullptr, delta,
+                       tile);
+          for (uint32_t r = 0; r < 8 && by * 8 + r < height; ++r)
+            std::memcpy(out + (size_t)(by * 8 + r) * out_pitch + bx * 8, tile + r * 8 * kGroup, 8 * kGroup);
+          bx += kGroup - 1;
+          continue;
+        }
         decode_block(flat.data(), codes, codes_bytes, block_offsets[b], block_init ? block_init[b] : 0,
                      delta, blk);
         const uint32_t nx = std::min(8u, width - bx * 8);
