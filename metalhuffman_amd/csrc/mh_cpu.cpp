@@ -48,11 +48,20 @@ inline mh_lookup_symbol split_lookup(const mh_lookup_symbol *t1, const mh_lookup
 
 // Every window's {symbol, width} from T1/T2 as one u16 (symbol | width << 8):
 // one lookup per symbol in the frame decoder.
+// Filled a T1 entry (256 windows) at a time: one value, or that entry's T2 subtable.
 void flatten(const mh_lookup_symbol *t1, const mh_lookup_symbol *t2, uint32_t t2_entries,
              uint16_t *flat) {
-  for (uint32_t p = 0; p < 65536; ++p) {
-    const mh_lookup_symbol e = split_lookup(t1, t2, t2_entries, p);
-    flat[p] = (uint16_t)(e.symbol | (e.bitWidth << 8));
+  for (uint32_t h = 0; h < 256; ++h) {
+    uint16_t *f = flat + h * 256u;
+    const mh_lookup_symbol e = t1[h];
+    if (e.bitWidth != 0) {
+      std::fill(f, f + 256, (uint16_t)(e.symbol | (e.bitWidth << 8)));
+    } else if ((uint32_t)e.symbol * MH_TABLE2_SIZE + 256u <= t2_entries) {
+      const mh_lookup_symbol *s = t2 + (uint32_t)e.symbol * MH_TABLE2_SIZE;
+      for (uint32_t l = 0; l < 256; ++l) f[l] = (uint16_t)(s[l].symbol | (s[l].bitWidth << 8));
+    } else {
+      std::fill(f, f + 256, (uint16_t)0);  // escape past T2: the zero entry (split_lookup)
+    }
   }
 }
 
