@@ -47,8 +47,8 @@ inline mh_lookup_symbol split_lookup(const mh_lookup_symbol *t1, const mh_lookup
 }
 
 // Every window's {symbol, width} from T1/T2 as one u16 (symbol | width << 8):
-// one lookup per symbol in the frame decoder.
-// Filled a T1 entry (256 windows) at a time: one value, or that entry's T2 subtable.
+// one lookup per symbol in the frame decoder, filled a T1 entry (256 windows) at a time:
+// one value, or that entry's T2 subtable.
 void flatten(const mh_lookup_symbol *t1, const mh_lookup_symbol *t2, uint32_t t2_entries,
              uint16_t *flat) {
   for (uint32_t h = 0; h < 256; ++h) {
@@ -187,7 +187,12 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
   if (out_pitch < width) return MH_ERR_CAPACITY;
   const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
-  std::vector<uint16_t> flat(65536);
+  std::vector<uint16_t> flat;
+  try {
+    flat.resize(65536);
+  } catch (...) {
+    return MH_ERR_CAPACITY;  // no exception crosses the C ABI
+  }
   flatten(table1, table2, table2_entries, flat.data());
   const auto rows = [&](uint32_t by0, uint32_t by1) {
     uint8_t blk[64];
