@@ -344,7 +344,9 @@ int mh_decode_huffman_bits_from_tables(const mh_lookup_symbol *table1, const mh_
  * offset with the shader's semantics (AAPLShaders.metal:241-268: 16-bit window,
  * T1/T2, delta fold unless MH_FLAG_NO_DELTA, optional per-block init byte), written
  * into the W x H raster at out_pitch; block rows split over n_threads host threads
- * (0 or 1: the calling thread). Bytes past codes_bytes read as zero. */
+ * (0 or 1: the calling thread); each thread decodes eight neighbouring blocks in
+ * lock-step. Bytes past codes_bytes read as zero. MH_ERR_CAPACITY if its 128 KB
+ * flat table cannot be allocated. */
 int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uint64_t codes_bytes,
                         const mh_lookup_symbol *table1, const mh_lookup_symbol *table2,
                         uint32_t table2_entries, const uint8_t *block_init, uint32_t width,
