@@ -343,8 +343,7 @@ int mh_decode_huffman_bits_from_tables(const mh_lookup_symbol *table1, const mh_
 /* The CPU twin of mh_decode for one frame: every 8x8 block from its root bit
  * offset with the shader's semantics (AAPLShaders.metal:241-268: 16-bit window,
  * T1/T2, delta fold unless MH_FLAG_NO_DELTA, optional per-block init byte), written
- * into the W x H raster at out_pitch; block rows shared out (one at a time, from a
- * counter) to n_threads host threads
+ * into the W x H raster at out_pitch; block rows split over n_threads host threads
  * (0 or 1: the calling thread); each thread decodes eight neighbouring blocks in
  * lock-step. Bytes past codes_bytes read as zero. MH_ERR_CAPACITY if its 128 KB
  * flat table cannot be allocated. */

@@ -11,7 +11,6 @@
 // 241-268, delta fold and init byte included) straight into the W x H raster,
 // block rows spread over host threads. None of these is called by the GPU path.
 #include <algorithm>
-#include <atomic>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -222,20 +221,20 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
     rows(0, bh);
     return MH_OK;
   }
-  // nt - 1 workers and the calling thread take block rows from a shared counter, so a
-  // worker that starts late (thread start-up is tens of us) simply takes fewer rows;
-  // no exception crosses the C ABI (a worker that cannot be started is not waited for)
-  std::atomic<uint32_t> next{0};
-  const auto work = [&] {
-    for (uint32_t by; (by = next.fetch_add(1, std::memory_order_relaxed)) < bh;) rows(by, by + 1);
-  };
+  // nt - 1 workers; the calling thread decodes the last share itself, and every
+  // share no worker could be started for (no exception crosses the C ABI)
   std::vector<std::thread> th;
+  uint32_t started = 0;
   try {
     th.reserve(nt - 1);
-    while (th.size() + 1 < nt) th.emplace_back(work);
+    for (; started + 1 < nt; ++started) {
+      const uint32_t a = (uint32_t)((uint64_t)bh * started / nt);
+      const uint32_t z = (uint32_t)((uint64_t)bh * (started + 1) / nt);
+      th.emplace_back(rows, a, z);
+    }
   } catch (...) {
   }
-  work();
+  rows((uint32_t)((uint64_t)bh * started / nt), bh);
   for (auto &x : th) x.join();
   return MH_OK;
 }
