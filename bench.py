@@ -8,14 +8,19 @@ Mpixel/s is the same number).
 A step is one pass of the hot path over one batch of input: by default
 (--workload frame, BASELINE config 2) one kernel launch that decodes one
 2048x1536 frame per GPU. Inputs are resident in HBM before timing starts: each
-rank holds --frames distinct block-shuffled BigBridge frames (the reference's
-own TEST_IMAGE4 asset; every shuffle shares one canonical table) and step i
-decodes frame i mod --frames, so repeated steps do not hit a warm cache
-(64 frames x 5.3 MB > the 256 MiB Infinity Cache). The K timed launches are
-captured in one hipGraph (HIP stream capture through torch.cuda.CUDAGraph) and
-replayed. Per-launch kernel durations (the roofline's denominator) come from HIP
-event pairs on the launch stream around the same launches issued eagerly right
-after the timed region (HIP does not time events recorded inside a capture).
+rank holds --frames (128) distinct block-shuffled BigBridge frames (the reference's
+own TEST_IMAGE4 asset; every shuffle shares one canonical table).
+
+Every clocked region is COLD, as every frame of the reference's renderer is new data
+(Shared/AAPLRenderer.m:1178-1921): it decodes frames no earlier region touched (the
+K eager launches of a region take the next K resident frames; the long launches --
+the 64-frame batch, the 8192^2 frame -- cycle over >= 2 launches of >= 337 MB), and
+a 1 GiB device copy evicts the 256 MiB Infinity Cache and the L2s right before the
+region, off the clock. The previous rounds' warm method (the clocked region
+re-decodes the frames the region before it decoded) is reported as `warm_value`.
+The K launches are enqueued behind a launch gate before the clock starts (short
+launches eagerly, long ones as hipGraph replays). `roofline.kernel_us_avg` is the
+timed region's own steady launch period from HIP events on the launch stream.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
 per GPU; rank 0 broadcasts the 256-byte canonical header over RCCL (xGMI) once and every
@@ -51,7 +56,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["frame", "batch", "tile8192", "tile8192_random"], default="frame")
-    ap.add_argument("--frames", type=int, default=64, help="distinct resident frames per rank")
+    ap.add_argument("--frames", type=int, default=128,
+                    help="distinct resident frames per rank (>= 2 batch launches: cold regions)")
     ap.add_argument("--batch", type=int, default=64, help="frames per launch for --workload batch")
     ap.add_argument("--no-extras", action="store_true", help="skip the batch/tile side measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -84,17 +90,36 @@ def algo_read_bytes(efs, t2_bytes: int) -> int:
     return sum(ef.payload_bytes + 4 * ef.n_blocks for ef in efs) + 512 + t2_bytes
 
 
-# A/B switch for decode-only flags (e.g. 2 = MH_FLAG_LANE_PAIRS); the parity guard
-# (Workload.verify) decodes through the same flags before anything is timed
+# A/B switch for decode-only flags (e.g. 2 = MH_FLAG_LANE_PAIRS, scripts/gpu_lane_pairs_ab.sh);
+# the parity guard (Workload.verify) decodes through the same flags before anything is timed
 DECODE_FLAGS = int(os.environ.get("MH_BENCH_DECODE_FLAGS", "0"), 0)
-# MH_BENCH_ANY_ORDER=1: inside an eager timed region every launch after the first goes
-# out with MH_FLAG_ANY_ORDER (no barrier bit: it may start while the previous frame's
-# decode drains; each launch writes its own raster). The first launch keeps the
-# barrier, so nothing starts before the region opens. On gfx950 the dispatches do not
-# overlap (scripts/micro/any_order_probe.hip); the gap between them shrinks: 5.56-5.62
+# Inside an eager timed region every launch after the first goes out with
+# MH_FLAG_ANY_ORDER (no barrier bit; each launch writes its own raster). The first launch
+# keeps the barrier, so nothing starts before the region opens. On gfx950 the dispatches
+# do not overlap (scripts/micro/any_order_probe.hip); the gap between them shrinks: 5.56-5.62
 # vs 5.78-5.82 us per launch over 20/64-launch regions (profiles/r02_v19_any_order_ab.txt).
-ANY_ORDER = os.environ.get("MH_BENCH_ANY_ORDER", "1") == "1"
 MH_FLAG_ANY_ORDER = 0x4
+FLUSH_BYTES = 512 << 20  # x2 buffers: 1 GiB of HBM traffic, 4x the 256 MiB Infinity Cache
+
+
+class _Flush:
+    """Evicts the Infinity Cache (MALL, 256 MiB) and the XCD L2s before a cold timed
+    region: one device copy of 512 MiB (512 MiB read + 512 MiB written), issued on the
+    launch stream before the region's opening synchronize, so it is off the clock."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def __call__(self, dev):
+        if dev not in self.bufs:
+            a = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
+            a.fill_(1)
+            self.bufs[dev] = (a, torch.empty_like(a))
+        a, b = self.bufs[dev]
+        b.copy_(a)
+
+
+FLUSH = _Flush()
 
 
 class Workload:
@@ -112,12 +137,14 @@ class Workload:
         self.bytes = bytes_per_launch
         self.read_bytes = read_bytes
         self.ungated_wall = None
+        self.warm_wall = None
         self.device = device
+        self.base = 0  # eager regions decode launches base, base+1, ... (advanced per cold region)
         self.outs = [torch.empty((f.n_frames, f.height, (f.width + 7) // 8 * 8), dtype=torch.uint8,
                                  device=device) for f in launches]
 
     def launch(self, i, stream=None, relaxed=False):
-        j = i % len(self.launches)
+        j = (self.base + i) % len(self.launches)
         self.D.decode(self.launches[j], self.tables, self.outs[j], stream=stream,
                       extra_flags=DECODE_FLAGS | (MH_FLAG_ANY_ORDER if relaxed else 0))
 
@@ -126,8 +153,9 @@ class Workload:
         i goes to stream i % nstreams (each launch still decodes one frame into its own
         buffer), all queued behind one launch gate per stream, opened together; the
         clock runs from the gate's opening to the closing synchronize. Independent
-        frames overlap on the device (one frame fills <= one wave per SIMD). Best of
-        `reps` regions -> seconds per launch."""
+        frames overlap on the device (one frame fills <= one wave per SIMD). Each region
+        decodes frames no earlier region touched, after the cache flush (cold inputs).
+        Best of `reps` regions -> seconds per launch."""
         dev = self.device
         if not GATE.ok():
             return None
@@ -135,6 +163,9 @@ class Workload:
         streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
         best = None
         for _ in range(reps + 1):  # the first region warms the streams
+            self.base = (self.base + steps) % len(self.launches)
+            self.base -= self.base % nstreams
+            FLUSH(dev)
             torch.cuda.synchronize(dev)
             for st in streams:
                 GATE.arm(st.cuda_stream)
@@ -155,6 +186,7 @@ class Workload:
         if self.refs is None:
             raise RuntimeError(f"{self.name}: no reference frames to verify against")
         n = 0
+        base, self.base = self.base, 0
         for j, fr in enumerate(self.launches):
             self.launch(j)
             torch.cuda.synchronize(self.device)
@@ -163,14 +195,25 @@ class Workload:
                 if not torch.equal(got[i], self.refs[j][i]):
                     raise SystemExit(f"bench: {self.name} launch {j} frame {i} differs from the encoder input")
                 n += 1
+        self.base = base
         return n
 
-    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=50.0, gate=True):
-        """Timed region: `steps` launches (one hipGraph replay, or eager), bracketed by
-        barrier + synchronize; wall = max over ranks.
-        Kernel durations: the same `steps` launches issued eagerly right after, each
-        bracketed by a pair of HIP events on the launch stream (HIP cannot record
-        timing events inside stream capture).
+    def check_outputs(self) -> None:
+        """After the timed regions: every launch's raster (as the any-order and rotated
+        regions left it) still equals its encoder input."""
+        for j, fr in enumerate(self.launches):
+            if not torch.equal(self.outs[j][..., : fr.width], self.refs[j]):
+                raise SystemExit(f"bench: {self.name} launch {j} differs from the encoder input after timing")
+
+    def run(self, steps, warmup, use_graph=True, world=1, settle_ms=50.0):
+        """Timed regions of `steps` launches each, bracketed by barrier + synchronize;
+        wall = max over ranks. Every clocked region is COLD: the launches it decodes were
+        not touched by the region before it (eager regions advance `base` by `steps`;
+        graph regions cycle over >= 2 launches of >= 337 MB each) and a 1 GiB copy evicts
+        the 256 MiB Infinity Cache and the L2s right before it (off the clock), as every
+        frame of the reference's renderer is new data (Shared/AAPLRenderer.m:1178-1921).
+        The previous warm method (the region re-decodes the frames the region before it
+        just decoded) is reported as `warm_wall`.
         -> (wall_s, gpu_region_ms, per-launch kernel ms list)."""
         dev = self.device
         for i in range(warmup):
@@ -185,22 +228,13 @@ class Workload:
         # rocprofv3 (78.3 vs 68.3 us batch, 30.4 vs 25.3 us 8192^2), which made the profile
         # disagree with the line (profiles/r03_window_ab.txt, r03_gate_rocprof_artifact.txt);
         # plain eager regions dispatch 5-8 % slower than queued ones
-        # (profiles/r03_long_launch_ab.txt). A launch of >= 113 MB leaves nothing warm in
-        # the 256 MiB Infinity Cache for the next replay of the same sequence. Short
-        # launches (one 2048x1536 frame, ~5.5 us) keep one graph of the K distinct launches
-        # (or eager launches behind the gate). Decided by size, not by a timing probe:
-        # under a profiler the probe itself slows.
-        # MH_BENCH_LONG (A/B): window (default) | graph (every replay behind the gate) |
-        # graph_ungated | eager
+        # (profiles/r03_long_launch_ab.txt). Short launches (one 2048x1536 frame, ~5.5 us)
+        # go out eagerly behind the gate. Decided by size, not by a timing probe: under a
+        # profiler the probe itself slows.
         self.long_launches = self.pixels >= LONG_LAUNCH_PIXELS
-        mode = os.environ.get("MH_BENCH_LONG", "window")
-        if self.long_launches and mode == "eager":
-            use_graph = gate = False
-        if self.long_launches and mode == "graph_ungated":  # A/B: the same replays, no gate
-            gate = False
-        window = self.long_launches and mode == "window"
+        window = self.long_launches
         G = steps  # launches per captured graph
-        if self.long_launches and mode in ("window", "graph", "graph_ungated") and steps % LONG_GRAPH_LAUNCHES == 0:
+        if self.long_launches and steps % LONG_GRAPH_LAUNCHES == 0:
             G = LONG_GRAPH_LAUNCHES
         self.graph_launches = G
         graph = None
@@ -236,36 +270,28 @@ class Workload:
             wb.record()
             torch.cuda.synchronize(dev)
             wa.elapsed_time(wb)
-        diag = int(os.environ.get("MH_BENCH_DIAG_REPEAT", "0"))  # diagnostics: spread of the timed region
-        for k in range(diag):
-            if graph is not None and settle_ms:
-                t_end = time.perf_counter() + settle_ms * 1e-3
-                while time.perf_counter() < t_end:
-                    replay_all()
-                    torch.cuda.synchronize(dev)
-            wa, wb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize(dev)
-            ta = time.perf_counter()
-            wa.record()
-            replay_all() if graph is not None else [self.launch(i) for i in range(steps)]
-            wb.record()
-            torch.cuda.synchronize(dev)
-            print(f"[diag] wall {(time.perf_counter() - ta) * 1e6:.1f} us", file=sys.stderr)
-        # eager behind the gate for short regions only: there the replayed graph's ~6 us
-        # start costs most; over 256 launches of the 64-frame batch the eager dispatches
-        # ran 68.2 vs 63.6 us each (graph), so long regions keep the replay
-        eager_gated = GATED_EAGER and steps <= 64 and not self.long_launches
-        def timed(gated, events=True, mark=False):
+        # eager behind the gate for short regions: there a replayed graph's ~6 us start
+        # costs most (profiles/r02_v10_gated_eager_vs_graph_ab.txt); long regions replay
+        eager_gated = steps <= 64 and not self.long_launches
+        G_unit = G if (graph is not None and not eager_gated) else 1
+
+        def timed(gated=True, events=True, mark=False, cold=True):
             """One timed region of exactly `steps` launches. Gated: the launches are
             enqueued behind the launch gate (scripts/micro/launch_gate.hip) after the
             opening synchronize, and the clock starts when the host opens it -- every
-            decode runs inside the region, the host's enqueue latency does not."""
+            decode runs inside the region, the host's enqueue latency does not.
+            cold: decode the next `steps` launches (eager) after the cache flush;
+            otherwise the same launches as the previous region, no flush (warm)."""
             r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             rA = torch.cuda.Event(enable_timing=True)  # after the region's first launch (or replay)
-            unit = G if (graph is not None and not (gated and eager_gated)) else 1
+            unit = G_unit if gated else (G if graph is not None else 1)
             if dist.is_initialized():
                 dist.barrier()
             st = torch.cuda.current_stream(dev).cuda_stream
+            if cold:
+                if eager_gated or graph is None:
+                    self.base = (self.base + steps) % len(self.launches)
+                FLUSH(dev)
             if mark and GATE.ok():
                 GATE.marker(st, 1)  # before the gate / the first launch: off the clock
             torch.cuda.synchronize(dev)
@@ -275,10 +301,10 @@ class Workload:
             # replays queued behind the gate (window mode: the first only, the rest are
             # enqueued once the gate is open, the host running ahead of the GPU)
             pre = nrep if not (gated and window) else min(1, nrep)
-            if gated or graph is not None:
+            if gated:
                 if events:
                     r0.record()
-                if graph is not None and not (gated and eager_gated):
+                if graph is not None and not eager_gated:
                     for r in range(pre):
                         graph.replay()
                         if r == 0 and events:
@@ -286,7 +312,7 @@ class Workload:
                 else:
                     # any-order only when every launch of the region writes its own raster
                     # (no launch may overlap one that writes the same buffer)
-                    relax = ANY_ORDER and len(self.launches) >= steps
+                    relax = len(self.launches) >= steps
                     for i in range(steps):
                         self.launch(i, relaxed=relax and i > 0)
                         if i == 0 and events:
@@ -311,12 +337,8 @@ class Workload:
                         if r == 0:
                             rA.record()
                 else:
-                    # diagnostics only (MH_BENCH_DIAG_RELAX=1): launches 2..K without the
-                    # barrier bit even over one raster (identical bytes) -- the A/B of what
-                    # a plain dispatch's barrier costs
-                    diag_relax = os.environ.get("MH_BENCH_DIAG_RELAX", "0") == "1"
                     for i in range(steps):
-                        self.launch(i, relaxed=diag_relax and i > 0)
+                        self.launch(i)
                         if i == 0:
                             rA.record()
                 r1.record()
@@ -336,35 +358,30 @@ class Workload:
                       (r0.elapsed_time(r1) / steps if events else None))
             return w, (r0.elapsed_time(r1) if events else None), (steady, unit)
 
-        if gate and GATE.ok():
-            timed(True)  # the gate's own first launch off the clock
+        if GATE.ok():
+            timed(events=False, cold=False)  # the gate's own first launch off the clock
+            # warm (the previous rounds' method, reported beside): the same launches again
+            self.warm_wall, _, _ = timed(events=False, cold=False)
             # The clocked region holds only the K launches: its two HIP event records
             # (markers in the queue) cost ~7 us per region at 20 steps (510 vs 482 x10^3
             # MB/s interleaved, profiles/r02_v13_region_events_ab.txt), so the event-timed
-            # region is a second, identical one. MH_BENCH_REGION_EVENTS=1 keeps them inside.
-            if os.environ.get("MH_BENCH_REGION_EVENTS", "0") == "0":
-                wall, _, _ = timed(True, events=False)
-                _, region_ms, (steady_ms, self.steady_unit) = timed(True, mark=True)
-            else:
-                wall, region_ms, (steady_ms, self.steady_unit) = timed(True, mark=True)
-            self.ungated_wall, _, _ = timed(False)
-            self.timed_launch = (("eager behind the launch gate" + (", launches 2..K with MH_FLAG_ANY_ORDER" if ANY_ORDER else ""))
+            # region is a second, identical (cold) one.
+            wall, _, _ = timed(events=False)
+            _, region_ms, (steady_ms, self.steady_unit) = timed(mark=True)
+            self.ungated_wall, _, _ = timed(gated=False)
+            self.timed_launch = (("eager behind the launch gate, launches 2..K with MH_FLAG_ANY_ORDER")
                                  if eager_gated else
-                                 (f"{steps // G} replays of a {G}-launch hipGraph, the first behind the launch gate, "
-                                  "the rest enqueued once it opens" if window else
-                                  f"{steps // G} replays of a {G}-launch hipGraph behind the launch gate"))
+                                 f"{steps // G} replays of a {G}-launch hipGraph, the first behind the launch gate, "
+                                 "the rest enqueued once it opens")
         else:
-            wall, region_ms, (steady_ms, self.steady_unit) = timed(False, mark=True)
+            wall, region_ms, (steady_ms, self.steady_unit) = timed(gated=False, mark=True)
             self.ungated_wall = None
-            self.timed_launch = ("hipGraph" if graph is not None else
-                                 "eager (long launches: the host enqueues ahead of the GPU)"
-                                 if self.long_launches else "eager")
-        # Per-launch kernel duration: the same K-launch graph replayed back to back
-        # (>= 200 launches) between one event pair on the launch stream, so the fixed
-        # cost of opening a region (gate release, first dispatch: ~13 us measured)
-        # is amortised as in rocprofv3's per-dispatch durations of the same launches.
+            self.timed_launch = "hipGraph" if graph is not None else "eager"
+        self.timed_launch += "; cold inputs (launches no earlier region touched, 1 GiB cache flush before each region)"
         self.region_kernel_ms = region_ms / steps
         self.steady_kernel_ms = steady_ms
+        # Per-launch kernel duration of the same launches replayed as graphs back to back
+        # (>= 200 launches, warm) between one event pair: informational.
         if graph is not None and G < steps:
             ka, kb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize(dev)
@@ -406,6 +423,7 @@ class Workload:
 
 
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+TILE_FRAMES = 6  # distinct 8192^2 frames per tile workload
 LONG_LAUNCH_PIXELS = 16 << 20  # Workload.run: launches decoding this many pixels are "long"
 LONG_GRAPH_LAUNCHES = 16       # ... and replay a graph of this many launches K / 16 times
 
@@ -428,15 +446,13 @@ ACHIEVABLE = {}  # filled from hbm_probe() before the roofline lines (rank 0, N=
 class _Gate:
     """The timed-region launch gate (scripts/micro/liblaunch_gate.so): a one-wave
     kernel polling a host-mapped flag, so the K launches can be enqueued before the
-    clock starts. MH_BENCH_GATE=0 times the plain (ungated) region only."""
+    clock starts."""
 
     def __init__(self):
         self.lib = None
         self.h = self.d = None
 
     def ok(self) -> bool:
-        if os.environ.get("MH_BENCH_GATE", "1") == "0":
-            return False
         if self.lib is None:
             import ctypes
             path = os.path.join(ROOT, "scripts", "micro", "liblaunch_gate.so")
@@ -468,15 +484,6 @@ class _Gate:
 
 
 GATE = _Gate()
-# Gated regions enqueue the K launches one by one (eager) rather than as one graph
-# replay: both are queued before the clock starts, but a replayed graph's first
-# kernel started ~6 us after the gate (rocprofv3 trace; a cross-queue wait), so at
-# the driver's 20 steps eager measured 477-483 vs 470-474 x10^3 MB/s interleaved on
-# one box (profiles/r02_v10_gated_eager_vs_graph_ab.txt). MH_BENCH_GATED_LAUNCH=graph
-# restores the replay.
-GATED_EAGER = os.environ.get("MH_BENCH_GATED_LAUNCH", "eager") == "eager"
-
-
 def roofline(bytes_per_launch, region_ms, steps, eager_ms=None, workload=None, read_bytes=None,
              kernel_ms=None, steady_ms=None, steady_unit=1):
     """achieved = algorithmic bytes of one launch / the launch's average duration,
@@ -680,6 +687,28 @@ def encode_rate(device, bb, reps=32):
         return (time.perf_counter() - t0) / reps
     pipe_s = in_flight(2)
     pipe4_s = in_flight(4)
+    # batched: 64 frames per call (mh_encode_frames_device_async, three launches),
+    # each frame its own tree; calls back to back on one stream, after a warm-up call
+    from metalhuffman_amd.encoder import BatchEncoder
+    nbatch = 64
+    benc = BatchEncoder(bb.shape[1], bb.shape[0], nbatch, device)
+    bimgs = torch.from_numpy(np.stack([F.block_shuffle(bb, 950 + k) for k in range(nbatch)])).to(device)
+    a = benc.encode_async(bimgs)
+    torch.cuda.synchronize(device)
+    if int((a.status != 0).sum().item()):
+        raise SystemExit("bench: batched encode rejected a frame")
+    for f in (0, nbatch - 1):  # parity guard: the host codec's bytes
+        ref = mh.encode_frame(bimgs[f].cpu().numpy())
+        if not np.array_equal(a.frame(f).codes.cpu().numpy(), ref.codes):
+            raise SystemExit("bench: batched encode differs from the host codec")
+    breps = 8
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(breps):
+        benc.encode_async(bimgs)
+    e1.record()
+    torch.cuda.synchronize(device)
+    batch_s = e0.elapsed_time(e1) * 1e-3 / (breps * nbatch)
     t0 = time.perf_counter()
     for k in range(4):
         mh.encode_frame(imgs[k])
@@ -697,6 +726,12 @@ def encode_rate(device, bb, reps=32):
             "gpu_async_2streams_ms_per_frame": round(pipe_s * 1e3, 3),
             "gpu_async_2streams_MBps": round(bb.size / pipe_s / 1e6, 1),
             "gpu_async_4streams_ms_per_frame": round(pipe4_s * 1e3, 3),
+            "gpu_batch64_ms_per_frame": round(batch_s * 1e3, 4),
+            "gpu_batch64_MBps": round(bb.size / batch_s / 1e6, 1),
+            "gpu_batch64_algorithmic_GBps": round(alg / batch_s / 1e9, 1),
+            "gpu_batch64_frac_of_8TBps": round(alg / batch_s / 8e12, 4),
+            "gpu_batch64_method": (f"{breps} calls of {nbatch} block-shuffled BigBridge frames back to back on one "
+                                   "stream (mh_encode_frames_device_async), HIP events, / frames"),
             "host_1thread_ms_per_frame": round(cpu_s * 1e3, 2), "host_1thread_MBps": round(bb.size / cpu_s / 1e6, 1)}
 
 
@@ -808,15 +843,14 @@ def main(argv=None) -> int:
     backend = os.environ.get("MH_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if os.environ.get("MH_BENCH_SYNC", "spin") == "spin":
-        # host waits spin (hipDeviceScheduleSpin) instead of yielding: the timed
-        # region's closing synchronize wakes without a scheduler round trip
-        # (single-shot 20-step walls: 138-147 us spin vs 141-177 us auto on one box,
-        # scripts/diag_timed_spread.sh). Set on this rank's device before its context.
-        import ctypes
-        hip = ctypes.CDLL("libamdhip64.so")
-        if hip.hipSetDevice(ctypes.c_int(local)) == 0:
-            hip.hipSetDeviceFlags(ctypes.c_uint(1))
+    # host waits spin (hipDeviceScheduleSpin) instead of yielding: the timed region's
+    # closing synchronize wakes without a scheduler round trip (single-shot 20-step
+    # walls: 138-147 us spin vs 141-177 us auto on one box, scripts/diag_timed_spread.sh).
+    # Set on this rank's device before its context.
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    if hip.hipSetDevice(ctypes.c_int(local)) == 0:
+        hip.hipSetDeviceFlags(ctypes.c_uint(1))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device")
     torch.cuda.set_device(local)
@@ -890,8 +924,10 @@ def main(argv=None) -> int:
         # config 3: BigBridge mirror tile (primary) or uniform random bytes (stress:
         # 8 bits/symbol, every code 8 bits, no T2 subtable), SURVEY.md 8(d)
         base = F.uniform_random(8192, 8192, 1234) if random else F.mirror_tile(bb, 8192, 8192)
-        imgs = [base] + [F.block_shuffle(base, 100 + k) for k in range(2)]
-        tefs = encode_many(imgs, threads=3)
+        # 6 distinct frames (680 MB of codes + offsets + rasters): a launch's inputs
+        # were last touched 5 launches earlier, far past the 256 MiB Infinity Cache
+        imgs = [base] + [F.block_shuffle(base, 100 + k) for k in range(TILE_FRAMES - 1)]
+        tefs = encode_many(imgs, threads=TILE_FRAMES)
         t1t, t2t = tefs[0].tables()
         ttabs = D.DeviceTables.upload(t1t, t2t, dev)
         launches = [pack([ef]) for ef in tefs]
@@ -924,10 +960,7 @@ def main(argv=None) -> int:
         ranks_ok = sum(1 for a, b in got if a == b)
 
     wall, region_ms, kms = wl.run(args.steps, args.warmup, use_graph=not args.no_graph, world=world)
-    if ANY_ORDER:  # the overlapped launches' rasters, as left by the timed regions
-        for j, fr in enumerate(wl.launches[:args.steps]):
-            if not torch.equal(wl.outs[j][..., : fr.width], wl.refs[j]):
-                raise SystemExit(f"bench: any-order launch {j} differs from the encoder input")
+    wl.check_outputs()  # the any-order / rotated regions' rasters
     per_step = wall / args.steps
     if not use_dist and not args.no_extras:
         ACHIEVABLE.update(hbm_probe() or {})  # after the timed region: the roofline context
@@ -950,6 +983,11 @@ def main(argv=None) -> int:
                    "the clock starts (scripts/micro/launch_gate.hip); every decode runs inside "
                    "the timed region" if wl.ungated_wall is not None else "plain"),
     }
+    if wl.warm_wall is not None:
+        # the previous rounds' method: the clocked region re-decodes the launches the
+        # region before it just decoded (inputs warm in the Infinity Cache)
+        result["warm_ms_per_step"] = round(wl.warm_wall / args.steps * 1e3, 5)
+        result["warm_value"] = round(world * wl.pixels / (wl.warm_wall / args.steps) / 1e6, 1)
     if wl.ungated_wall is not None:
         # the same K launches timed the plain way (enqueue latency inside the clock)
         result["ungated_ms_per_step"] = round(wl.ungated_wall / args.steps * 1e3, 5)
@@ -990,7 +1028,10 @@ def main(argv=None) -> int:
             w2 = make()
             nver = w2.verify()
             wall2, reg2, kms2 = w2.run(steps, steps, use_graph=not args.no_graph)
+            w2.check_outputs()
             extras[name] = {"value_MBps": round(w2.pixels / (wall2 / steps) / 1e6, 1),
+                            "warm_value_MBps": (round(w2.pixels / (w2.warm_wall / steps) / 1e6, 1)
+                                                if w2.warm_wall else None),
                             "ms_per_step": round(wall2 / steps * 1e3, 4),
                             "gpu_region_ms_per_step": round(reg2 / steps, 4),
                             "frames_verified": nver,

@@ -219,6 +219,34 @@ int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t heigh
                            uint64_t *codes_len, uint32_t *d_block_offsets, uint8_t *d_block_init,
                            void *d_workspace, size_t workspace_bytes, void *stream);
 
+/* Device workspace mh_encode_frames_device_async needs for n_frames frames of
+ * width x height. */
+size_t mh_encode_frames_workspace_bytes(uint32_t width, uint32_t height, uint32_t n_frames);
+
+/* Batched GPU encode: n_frames independent frames of one size (frame f's pixels at
+ * d_gray + f * gray_frame_stride, rows of W bytes), each with its OWN histogram,
+ * Huffman tree, canonical header and codes -- byte-identical, frame by frame, to
+ * mh_encode_frame (HuffmanEncoder.cpp:310-381, HuffmanUtil.cpp:1051-1131) -- in
+ * three launches whatever n_frames (tiled split; one tree workgroup per frame, which
+ * also turns the frame's per-tile symbol counts into tile bit offsets; packing), so
+ * frames no longer queue behind one workgroup's tree each. Outputs, per frame f:
+ * d_canon_headers + 256 f, codes at d_codes + f * codes_frame_stride (16-byte
+ * aligned slots; the slot size is the capacity), d_codes_len[f] (optional),
+ * d_block_offsets + f * NB, d_block_init + f * NB (optional), d_status[f]
+ * (optional; the values of mh_encode_frame_device_async), and d_frame_code_offsets
+ * (optional, n_frames + 1 u64 = f * codes_frame_stride): the slots are then one
+ * mh_frame batch for mh_decode (all frames must share one canonical table to be
+ * decoded in one launch, e.g. block shuffles of one image). A rejected frame writes
+ * no codes or offsets and does not affect the others. d_workspace: 256-byte aligned,
+ * mh_encode_frames_workspace_bytes(); MH_ENCODE_WORKSPACE_ZEROED as for
+ * mh_encode_frame_device_async (every call leaves the histograms zeroed).
+ * Asynchronous on `stream`; the return value covers argument checks and launches. */
+int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_stride, uint32_t n_frames,
+                                  uint32_t width, uint32_t height, uint32_t flags, uint8_t *d_canon_headers,
+                                  uint8_t *d_codes, uint64_t codes_frame_stride, uint64_t *d_codes_len,
+                                  uint64_t *d_frame_code_offsets, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                                  int32_t *d_status, void *d_workspace, size_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Streaming from host memory (BASELINE config 5; the reference's per-frame  */
 /* command buffer, AAPLRenderer.m:1178-1921).                               */

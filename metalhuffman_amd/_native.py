@@ -32,7 +32,7 @@ EXPORTS = (
     "mh_stream_group_create", "mh_stream_group_submit", "mh_stream_group_member", "mh_stream_group_size",
     "mh_stream_group_synchronize", "mh_stream_group_destroy",
     "mh_code_lengths", "mh_encode_workspace_bytes", "mh_encode_frame_device",
-    "mh_encode_frame_device_async",
+    "mh_encode_frame_device_async", "mh_encode_frames_workspace_bytes", "mh_encode_frames_device_async",
     "mh_container_header", "mh_parse_container_header", "mh_check",
     "mh_decode_huffman_bits", "mh_decode_huffman_bits_from_tables", "mh_decode_frame_cpu",
     "mh_build_stamp",
@@ -135,6 +135,11 @@ def lib() -> ctypes.CDLL:
         L.mh_encode_frame_device_async.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                    _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                                    ctypes.c_size_t, _vp]
+        L.mh_encode_frames_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.mh_encode_frames_workspace_bytes.restype = ctypes.c_size_t
+        L.mh_encode_frames_device_async.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                                    _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]
         L.mh_split_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint8, _u8p, ctypes.c_size_t]
         L.mh_merge_blocks.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,

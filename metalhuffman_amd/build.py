@@ -96,7 +96,16 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     """Rebuild by CONTENT, not mtime (a snapshot may carry any mtimes), and link the
-    library with its stamp compiled in, so the loader can refuse a stale one."""
+    library with its stamp compiled in, so the loader can refuse a stale one.
+
+    A library whose stamp equals the tree's (every source, header and flag) is
+    current: nothing is compiled or linked. That is the GPU box's case -- the library
+    is built here, in the build container, and travels with the snapshot (objects in
+    _build/ do not); the box only checks the stamp, and _native.lib() refuses to load
+    a library whose compiled-in stamp differs from the tree's sources."""
+    lst = library_stamp()
+    if not force and _stamp_ok(LIB, lst):
+        return LIB
     os.makedirs(BUILD, exist_ok=True)
     objs = []
     for obj, (src, cmd) in SOURCES.items():
@@ -110,7 +119,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 print(" ".join(full), flush=True)
             subprocess.run(full, check=True)
             _write_stamp(obj_path, st)
-    lst = library_stamp()
     if force or not _stamp_ok(LIB, lst):
         stamp_c = os.path.join(BUILD, "mh_stamp.c")
         with open(stamp_c, "w") as f:
@@ -133,7 +141,6 @@ DIAG_DIR = os.path.join(PKG, "diag")
 # flags, the objects they change; the rest are the default build's objects)
 DIAG_LIBS = {
     "spin0": (["MH_DIAG_SPIN_TICKS=0"], ["mh_encode.o"]),  # encoder packers time out at once
-    "claim0": (["MH_ONE_CLAIM_TICKS=0"], ["mh_encode.o"]),  # encoder workgroup 0 claims tiles at once
 }
 
 
@@ -226,6 +233,25 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return HOST_BIN
 
 
+MULTI_SRC = os.path.join(ROOT, "host", "mh_decode_multi.c")
+MULTI_BIN = os.path.join(ROOT, "host", "mh_decode_multi")
+
+
+def build_host_multi(force: bool = False, verbose: bool = False) -> str:
+    """The plain-C multi-GPU host (host/mh_decode_multi.c): one thread per device,
+    RCCL broadcast of the 256-byte canonical header, batched device encode and decode."""
+    lib = build(force=force, verbose=verbose)
+    if force or _stale(MULTI_BIN, [MULTI_SRC, lib] + HEADERS):
+        cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-pthread", "-D__HIP_PLATFORM_AMD__",
+               "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROCM, "include"), MULTI_SRC,
+               "-o", MULTI_BIN, "-L", PKG, "-lmetalhuffman_amd", "-L", os.path.join(ROCM, "lib"),
+               "-lrccl", "-lamdhip64", f"-Wl,-rpath,$ORIGIN/../metalhuffman_amd:{os.path.join(ROCM, 'lib')}"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return MULTI_BIN
+
+
 PROBE_SRC = os.path.join(ROOT, "scripts", "micro", "hbm_probe.hip")
 PROBE_LIB = os.path.join(ROOT, "scripts", "micro", "libhbm_probe.so")
 GATE_SRC = os.path.join(ROOT, "scripts", "micro", "launch_gate.hip")
@@ -252,6 +278,7 @@ def main(argv=None) -> int:
     print(build(force=args.force, verbose=True))
     print(build_diag(force=args.force, verbose=True))
     print(build_host(force=args.force, verbose=True))
+    print(build_host_multi(force=args.force, verbose=True))
     print(build_probe(force=args.force, verbose=True))
     return 0
 

@@ -9,9 +9,14 @@
 // symbol's bit offset. mh_decode_frame_cpu is the CPU twin of mh_decode: the
 // shader semantics per 8x8 block from its root bit offset (AAPLShaders.metal:
 // 241-268, delta fold and init byte included) straight into the W x H raster,
-// block rows spread over host threads. None of these is called by the GPU path.
+// block rows spread over a persistent pool of host threads (started on first use,
+// reused by every later call). None of these is called by the GPU path.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -135,6 +140,85 @@ inline void decode_group(const uint16_t *flat, const uint8_t *codes, const uint3
     }
 }
 
+// Persistent worker pool for mh_decode_frame_cpu. Round 3 started fresh threads on
+// every call: 16 threads reached 5.6 x10^3 MB/s best-of but ~3.5-4.0 x10^3 per call in
+// the bench line. Workers are started once (grown on demand, never shrunk) and sleep
+// on a condition variable between calls; a call hands out job indices from an atomic
+// counter to its first n - 1 workers and the calling thread. One parallel call runs
+// at a time (calls from several host threads queue on run_mutex_). No exception
+// crosses the C ABI: a worker that cannot be started leaves its share to the others.
+class Pool {
+ public:
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_) t.join();
+  }
+
+  // fn(j) for j in [0, njobs) on up to `threads` threads (the caller included).
+  void run(uint32_t threads, uint32_t njobs, const std::function<void(uint32_t)> &fn) {
+    std::lock_guard<std::mutex> call(run_mutex_);
+    const uint32_t want = threads > 1 ? threads - 1 : 0;
+    try {
+      while (workers_.size() < want) {
+        const uint32_t id = (uint32_t)workers_.size();
+        workers_.emplace_back([this, id] { loop(id); });
+      }
+    } catch (...) {
+    }
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      njobs_ = njobs;
+      next_.store(0, std::memory_order_relaxed);
+      active_ = std::min<uint32_t>(want, (uint32_t)workers_.size());
+      busy_ = active_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (uint32_t j; (j = next_.fetch_add(1, std::memory_order_relaxed)) < njobs_;) (*fn_)(j);
+  }
+  void loop(uint32_t id) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && id < active_); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--busy_ == 0) done_cv_.notify_one();
+    }
+  }
+
+  std::mutex run_mutex_, m_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(uint32_t)> *fn_ = nullptr;
+  uint32_t njobs_ = 0, active_ = 0, busy_ = 0;
+  std::atomic<uint32_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+Pool &pool() {
+  static Pool p;
+  return p;
+}
+
 }  // namespace
 
 extern "C" {
@@ -216,26 +300,20 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
           std::memcpy(out + (size_t)(by * 8 + r) * out_pitch + bx * 8, blk + r * 8, nx);
       }
   };
-  uint32_t nt = std::max(1u, std::min(n_threads ? n_threads : 1u, bh));
+  const uint32_t nt = std::max(1u, std::min(n_threads ? n_threads : 1u, bh));
   if (nt == 1) {
     rows(0, bh);
     return MH_OK;
   }
-  // nt - 1 workers; the calling thread decodes the last share itself, and every
-  // share no worker could be started for (no exception crosses the C ABI)
-  std::vector<std::thread> th;
-  uint32_t started = 0;
+  // nt contiguous shares of block rows on the persistent pool (the caller takes one)
   try {
-    th.reserve(nt - 1);
-    for (; started + 1 < nt; ++started) {
-      const uint32_t a = (uint32_t)((uint64_t)bh * started / nt);
-      const uint32_t z = (uint32_t)((uint64_t)bh * (started + 1) / nt);
-      th.emplace_back(rows, a, z);
-    }
+    const std::function<void(uint32_t)> job = [&](uint32_t j) {
+      rows((uint32_t)((uint64_t)bh * j / nt), (uint32_t)((uint64_t)bh * (j + 1) / nt));
+    };
+    pool().run(nt, nt, job);
   } catch (...) {
+    return MH_ERR_CAPACITY;  // no exception crosses the C ABI
   }
-  rows((uint32_t)((uint64_t)bh * started / nt), bh);
-  for (auto &x : th) x.join();
   return MH_OK;
 }
 

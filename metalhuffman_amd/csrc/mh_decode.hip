@@ -33,71 +33,18 @@
 
 namespace {
 
-#ifndef MH_MAX_WAVES
-#define MH_MAX_WAVES 8
-#endif
-#ifndef MH_DIAG_BROADCAST_LUT   // diagnostic builds only: every lane reads LUT entry 0 (wrong output)
-#define MH_DIAG_BROADCAST_LUT 0
-#endif
-#ifndef MH_MIN_WAVES_PER_EU     // register cap: 6 waves/SIMD = what the LDS budget admits
-#define MH_MIN_WAVES_PER_EU 6
-#endif
-#ifndef MH_ROW_UNROLL           // 8: straight-line decode, so vmcnt can count the row stores
-#define MH_ROW_UNROLL 8
-#endif
-#ifndef MH_NT_STORE
-#define MH_NT_STORE 1
-#endif
-#ifndef MH_STORE_AUX            // batch kernel row-store cache bits (gfx950 aux: 1 sc0, 2 nt, 16 sc1)
-#define MH_STORE_AUX (MH_NT_STORE ? 2 : 0)
-#endif
-#ifndef MH_REFILL_PIN           // 1: pin the masked refill's hi/lo selects before the read
-#define MH_REFILL_PIN 1
-#endif
-#ifndef MH_SMALL_STORE_AUX      // small-launch kernel: nt sc1, write-through (nothing dirty is left
-#define MH_SMALL_STORE_AUX 18   //    in the XCDs' L2s for the end-of-kernel release to write back)
-#endif
-#ifndef MH_SPEC_REFILL          // 1: refill folded into the pair's first lookup (A/B)
-#define MH_SPEC_REFILL 0
-#endif
-#ifndef MH_PRIO_ROTATE          // wave priority: 0 off, 1 rotate per tile, 2 per block row,
-#define MH_PRIO_ROTATE 3        // 3 by remaining tiles (default)
-#endif
-#ifndef MH_PERM3                // 1: assemble output words from 4 lane states (3 VALU / 4 bytes)
-#define MH_PERM3 1
-#endif
-#ifndef MH_SMALL_KERNEL         // 1: launches of <= 4 tiles per CU use mh_decode_small_kernel
-#define MH_SMALL_KERNEL 1
-#endif
-#ifndef MH_STAGE_SWIZZLE        // 1: flat tables (one code length) stage chunks XOR-permuted
-#define MH_STAGE_SWIZZLE 1      //    within 128-B rows (batch kernel)
-#endif
-#ifndef MH_NOESC_PATH           // 1: batch kernel steps without the escape test when the
-#define MH_NOESC_PATH 1         //    prepared table's longest code is <= 13 bits
-#endif
-#ifndef MH_MASKED_REFILL        // 1: in the batch kernel, only lanes that consumed a word
-#define MH_MASKED_REFILL 1      //    read the next one (fewer LDS bank conflicts)
-#endif
-#ifndef MH_SMALL_SPEC           // small-launch kernel step: 1 refill off the chain (kSpec; 1.2 % slower)
-#define MH_SMALL_SPEC 0
-#endif
-#ifndef MH_SMALL_MASKED         // small-launch kernel: masked refill reads (kSpec 0 only)
-#define MH_SMALL_MASKED 0
-#endif
-#ifndef MH_LP_MIN_BITS          // lane-pair variant: blocks shorter than 2x this decode on one lane
-#define MH_LP_MIN_BITS 16
-#endif
-#ifndef MH_LUT_FIRST            // 1: batch kernel issues the table's loads before the first header (A/B)
-#define MH_LUT_FIRST 0
-#endif
-#ifndef MH_TLB_PREFETCH         // 1: the small kernel touches its code and raster pages at wave
-#define MH_TLB_PREFETCH 0       //    start, beside the block-offset load (translation warm-up, A/B)
-#endif
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
-#define MH_DIAG_STAMPS 0
+#define MH_DIAG_STAMPS 0        //    (scripts/diag_stamps.py)
 #endif
 constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile span)
-constexpr int kMaxWavesPerWG = MH_MAX_WAVES;
+constexpr int kMaxWavesPerWG = 8;             // batch kernel workgroup width
+constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = what the LDS budget admits
+// Row-store cache bits (gfx950 aux field: 1 sc0, 2 nt, 16 sc1). Batch kernel: nt.
+// Small-launch kernel: nt sc1, write-through, so nothing dirty is left in the XCDs'
+// L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt).
+constexpr int kBatchStoreAux = 2;
+constexpr int kSmallStoreAux = 18;
+constexpr uint32_t kLpMinBits = 16;           // lane-pair variant: blocks shorter than 2x this decode on one lane
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
@@ -191,7 +138,7 @@ struct LdsWords {
   const uint8_t *w;
   __device__ __forceinline__ const uint8_t *at(uint32_t byte_off) const { return w + byte_off; }
 };
-// Stage swizzle (batch kernel, MH_STAGE_SWIZZLE): the eight 16-B chunks of every
+// Stage swizzle (batch kernel, flat tables only): the eight 16-B chunks of every
 // 128-B row of a wave's stage are permuted by the row index (XOR), so lanes whose
 // blocks start a multiple of 128 B apart -- flat code lengths make every block
 // exactly 64 B -- refill from different LDS banks (b32 reads bank on (a/4) mod 32).
@@ -224,8 +171,8 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 
 // Wave priority 0..3 (s_setprio takes an immediate). The SIMD arbiter serves the
 // oldest wave first among equal priorities, so waves of later workgroups fall
-// behind; rotating every wave through all four levels evens out their progress.
-[[maybe_unused]] __device__ __forceinline__ void set_prio(uint32_t p) {
+// behind; the batch loop gives waves with more tiles left a higher priority.
+__device__ __forceinline__ void set_prio(uint32_t p) {
   switch (__builtin_amdgcn_readfirstlane(p) & 3u) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
     case 1: __builtin_amdgcn_s_setprio(1); break;
@@ -238,30 +185,27 @@ __device__ unsigned long long g_stamps[kDiagWaves * kDiagSlots];
 //   Lut13: 2^13-entry first level + escapes to the second level (any code <= 16 bits).
 //   Lut14: 2^14-entry single level, no escape test at all; valid when no code is
 //          longer than 14 bits (the prepared table records the longest code).
-// kSpec: the table address of a pair's first symbol is taken from whichever
-//   window the refill selects (two shifts in parallel), taking the word move off
-//   the dependency chain: +2 VALU per pair for a shorter per-symbol latency.
-template <int kBits, bool kSpecRefill, bool kMaskedRefill = false, bool kEscapes = kBits == kLutBits,
-          bool kSwizzle = false, int kStoreAux = MH_STORE_AUX>
+// kMasked: only the lanes that consumed a word read the next one (batch kernel);
+//   the small-launch kernel's latency-bound chain reads unmasked.
+template <int kBits, bool kMaskedRefill, bool kEscapes = kBits == kLutBits, bool kSwizzle = false,
+          int kStoreAux = kBatchStoreAux>
 struct StepCfg {
   static constexpr int kAux = kStoreAux;  // row-store cache bits
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
-  static constexpr bool kSpec = kSpecRefill;
-  static constexpr bool kMasked = kMaskedRefill && !kSpecRefill;
+  static constexpr bool kMasked = kMaskedRefill;
   static constexpr uint32_t kCur = 127u - (uint32_t)kBits;   // S low byte = kCur - sh
   static constexpr uint32_t kMask = (2u << kBits) - 2u;       // byte address of a u16 entry
   static constexpr uint32_t kRefillAt = kCur - 32u;           // low byte <= this: sh >= 32
 };
 
-using Lut13 = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0>;  // the batch kernel's step
+using Lut13 = StepCfg<kLutBits, true>;  // the batch kernel's step
 // ... and its escape-free twin, for tables whose longest code is <= 13 bits (the
 // first level then decodes every window; no per-symbol escape test)
-using Lut13NoEsc = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false>;
+using Lut13NoEsc = StepCfg<kLutBits, true, false>;
 // ... and for flat tables (every code the same length, e.g. uniform bytes: every
 // block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
-using Lut13Flat = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, false,
-                          MH_STAGE_SWIZZLE != 0>;
+using Lut13Flat = StepCfg<kLutBits, true, false, true>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -277,8 +221,7 @@ using Lut13Flat = StepCfg<kLutBits, MH_SPEC_REFILL != 0, MH_MASKED_REFILL != 0, 
 template <bool kDelta, class Cfg, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut, uint32_t p,
                                              uint32_t prev, __amdgpu_buffer_rsrc_t out,
-                                             uint32_t row0, uint32_t pitch, bool dead,
-                                             uint32_t prio = 0) {
+                                             uint32_t row0, uint32_t pitch, bool dead) {
   // wa: LDS address of hi's word in the staged span. An explicit local-address-space
   // pointer keeps its arithmetic 32-bit (a generic pointer was carried as a 64-bit value:
   // one 64-bit add per refill) and lets the reads fold their constant offsets.
@@ -301,17 +244,10 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   uint32_t hi = rd(wa);
   uint32_t lo = rd(wa + 4);
   uint32_t nw = rd(wa + 8);
-  (void)prio;
-  // MH_DIAG_BROADCAST_LUT: every lookup address ANDed with an opaque zero, so the read
-  // stays on the chain (a literal 0 let the compiler hoist it out of the loop) but every
-  // lane reads entry 0: conflict-free broadcasts, wrong output (diagnostic builds only)
-  uint32_t diag_zero = 0;
-  if constexpr (MH_DIAG_BROADCAST_LUT != 0) asm volatile("v_mov_b32 %0, 0" : "=v"(diag_zero));
-  (void)diag_zero;
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_LOOKUP(A1)                                                               \
-  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (MH_DIAG_BROADCAST_LUT ? (A1) & diag_zero : (A1)));
+  uint32_t e = *reinterpret_cast<const uint16_t *>(lut + (A1));
 #define MH_FINISH(J, OW)                                                            \
   {                                                                                 \
     if constexpr (Cfg::kEsc) {                                                      \
@@ -326,7 +262,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     }                                                                               \
     S += e;                                                                         \
     if (kDelta) {                                                                   \
-      if (MH_PERM3) sv[J] = S; else OW = __builtin_amdgcn_perm(S, OW, ins_sel1(J));  \
+      sv[J] = S;  /* packed four at a time (pack_prev4) */                         \
     } else {                                                                        \
       OW = __builtin_amdgcn_perm(e + 0xFFu, OW, ins_sel1(J));  /* byte 1: symbol */  \
     }                                                                               \
@@ -350,44 +286,29 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     /* masked refill: the selects stay selects (v_cndmask) -- else the compiler   */  \
     /* folds them into the masked read's if-block as exec-masked copies (8 moves  */  \
     /* at every row start)                                                        */  \
-    if constexpr (Cfg::kMasked && MH_REFILL_PIN) asm volatile("" : "+v"(hi), "+v"(lo)); \
+    if constexpr (Cfg::kMasked) asm volatile("" : "+v"(hi), "+v"(lo));             \
     S += d * 8u;                                                                    \
     if constexpr (!Cfg::kMasked) nw = rd(wa + 8);                                   \
   }
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
     const bool c = (S & 0xFFu) <= kRefill;                                         \
-    if constexpr (Cfg::kSpec) {                                                     \
-      const uint32_t v0 = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (S & 63u));  \
-      const uint32_t v1 = (uint32_t)(((((uint64_t)lo) << 32) | nw) >> ((S + 32u) & 63u)); \
-      MH_LOOKUP((c ? v1 : v0) & Cfg::kMask)                                         \
-      MH_REFILL_C(c)                                                                \
-      MH_FINISH(J, OW)                                                              \
-    } else {                                                                        \
-      MH_REFILL_C(c)                                                                \
-      MH_STEP(J, OW)                                                                \
-      /* masked: only lanes that consumed a word fetch the next (issued behind */   \
-      /* the lookup; fewer active lanes -> fewer LDS bank conflicts)          */   \
-      if constexpr (Cfg::kMasked) {                              \
-        if (c) nw = rd(wa + 8);                                                     \
-      }                                                                             \
+    MH_REFILL_C(c)                                                                  \
+    MH_STEP(J, OW)                                                                  \
+    /* masked: only lanes that consumed a word fetch the next (issued behind the */ \
+    /* lookup; fewer active lanes -> fewer LDS bank conflicts)                   */ \
+    if constexpr (Cfg::kMasked) {                                                   \
+      if (c) nw = rd(wa + 8);                                                       \
     }                                                                               \
   }
 
   // dead lanes store at >= 2^31 + r * pitch: past every output descriptor's range
   // (<= 0x7FFFFFF0 bytes), so the hardware drops them -- one select per tile, not per row
   const uint32_t rbase = dead ? 0x80000000u : row0;
-#if MH_ROW_UNROLL == 8
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
   for (uint32_t r = 0; r < 8; ++r) {
-#if MH_PRIO_ROTATE == 2
-    set_prio(prio + r);
-#endif
     uint32_t o0 = 0, o1 = 0;
-    uint32_t sv[4];  // MH_PERM3: S after each symbol of the current output word
+    uint32_t sv[4];  // S after each symbol of the current output word (delta mode)
     (void)sv;
     if (r) {
       MH_STEP_R(0, o0);
@@ -397,12 +318,12 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     MH_STEP(1, o0);
     MH_STEP_R(2, o0);
     MH_STEP(3, o0);
-    if (MH_PERM3 && kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    if (kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
     MH_STEP_R(0, o1);
     MH_STEP(1, o1);
     MH_STEP_R(2, o1);
     MH_STEP(3, o1);
-    if (MH_PERM3 && kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    if (kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
     // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
     // block and rows below the frame use offsets outside the descriptor's range,
     // which the hardware drops. A right-edge block writes its 8 bytes into the
@@ -660,37 +581,10 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
 #endif
   MH_STAMP(0);
 
-  uint32_t prio = blockIdx.x * nwaves + wave;  // rotation phase (MH_PRIO_ROTATE 1, 2)
   // static grid-stride schedule; a tile id >= total_tiles means "no tile"
   const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
-#if MH_LUT_FIRST
-  // The table's L2 loads go out before the first header's HBM load, so waiting for
-  // them (vmcnt counts in issue order) does not wait for the header: the table is in
-  // LDS, and the workgroup barrier passed, while the headers are still in flight.
-  constexpr uint32_t kLutChunks = kLutBytes / 16, kLutPer = 4;
-  const bool lut_regs = a.lut && blockDim.x * kLutPer >= kLutChunks;  // >= 5 waves
-  if (lut_regs) {
-    const __amdgpu_buffer_rsrc_t rl = uniform_rsrc(a.lut, (uint32_t)kLutBytes);
-    v4u32 L[kLutPer];
-#pragma unroll
-    for (uint32_t k = 0; k < kLutPer; ++k)
-      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * blockDim.x) * 16u), 0, 0);
-    hdr_issue(a, t0, lane, hc);
-    v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-#pragma unroll
-    for (uint32_t k = 0; k < kLutPer; ++k)
-      if (threadIdx.x + k * blockDim.x < kLutChunks) dstv[threadIdx.x + k * blockDim.x] = L[k];
-  } else {
-    hdr_issue(a, t0, lane, hc);
-    if (a.lut) {
-      const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
-      v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-      for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
-    }
-  }
-#else
   hdr_issue(a, t0, lane, hc);
 
   // ---- lookup table into LDS (shared by the workgroup) ----
@@ -699,7 +593,6 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
     for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
   }
-#endif
 
   v4u32 R[kStageChunks];
   Tile cur = hdr_resolve(a, hc, lane);
@@ -736,15 +629,9 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
       const __amdgpu_buffer_rsrc_t out = ot.rsrc;
       const uint32_t row0 = ot.row0;
       LdsWords src{stage};
-#if MH_PRIO_ROTATE == 1
-      set_prio(prio);
-#elif MH_PRIO_ROTATE == 3
       // waves with more tiles left run first (the arbiter otherwise favours the oldest)
       set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
-#endif
-      decode_block<kDelta, Cfg>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead,
-                                prio);
-      prio += MH_PRIO_ROTATE == 2 ? 3u : 1u;
+      decode_block<kDelta, Cfg>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
     }
 #if MH_DIAG_STAMPS
     if (first_tile) MH_STAMP(4);
@@ -786,16 +673,16 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
 // than 13 bits -> escape-free; one code length only -> escape-free with the
 // swizzled stage. An in-kernel table (no prepared LUT) keeps the general step.
 template <bool kDelta>
-__global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_decode_kernel(const DecodeArgs a) {
+__global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(const DecodeArgs a) {
   uint32_t mx = 16, mn = 0;
   if (a.lut) {
     const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
     mx = ml[0];
     mn = ml[1];
   }
-  if (MH_STAGE_SWIZZLE && a.lut && mx == mn)
+  if (a.lut && mx == mn)
     batch_tiles<kDelta, Lut13Flat>(a);
-  else if (MH_NOESC_PATH && a.lut && mx <= (uint32_t)kLutBits)
+  else if (a.lut && mx <= (uint32_t)kLutBits)
     batch_tiles<kDelta, Lut13NoEsc>(a);
   else
     batch_tiles<kDelta, Lut13>(a);
@@ -808,10 +695,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, MH_MIN_WAVES_PER_EU) mh_d
 // single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
-#ifndef MH_SMALL_WAVES
-#define MH_SMALL_WAVES 4
-#endif
-constexpr int kSmallWaves = MH_SMALL_WAVES;  // waves per workgroup (one tile each)
+constexpr int kSmallWaves = 4;  // waves per workgroup (one tile each)
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
@@ -833,26 +717,6 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr h;
   hdr_issue(a, tile, lane, h);
-#if MH_TLB_PREFETCH
-  // Translation warm-up: one load from the page of the code bytes this tile most likely
-  // starts in (its share of the frame's bytes; only the address's page matters, the
-  // value is never used) and one from its first raster row, issued beside the
-  // block-offset load so the three page walks overlap instead of following each other.
-  uint32_t warm = 0;
-  {
-    const uint32_t tf = a.total_tiles <= a.tiles_per_frame ? tile : tile % a.tiles_per_frame;
-    const uint32_t fb = (uint32_t)min<uint64_t>(a.codes_bytes, 0xFFFFFFF0ull);
-    const uint32_t est = (uint32_t)(((uint64_t)tf * fb) / a.tiles_per_frame) & ~63u;
-    const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(a.codes, a.frame_off ? 0u : fb);
-    const uint32_t by0 = (tf * 64u) / a.bw;
-    const uint64_t ro = (uint64_t)by0 * 8u * a.out_pitch;
-    const __amdgpu_buffer_rsrc_t rw = uniform_rsrc(a.out, ro < a.out_frame_bytes ? 0x7FFFFFF0u : 0u);
-    if (lane == 0) {
-      warm = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)est, 0, 0);
-      warm += __builtin_amdgcn_raw_buffer_load_b32(rw, (int)(uint32_t)min<uint64_t>(ro, 0x7FFFFF00ull), 0, 0);
-    }
-  }
-#endif
   const bool l14 = max_len <= (uint32_t)kLut14Bits;
   // Table copy: a fixed count of unconditional 16-B loads per thread (chunks past
   // the table fall outside the descriptor), issued behind the offsets so that the
@@ -886,10 +750,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
   const uint32_t row0 = ot.row0;
   // the small kernel's step flavours (all with write-through row stores)
-  using Small14 = StepCfg<kLut14Bits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0, false, false, MH_SMALL_STORE_AUX>;
-  using Small13 = StepCfg<kLutBits, MH_SMALL_SPEC != 0, MH_SMALL_MASKED != 0, true, false, MH_SMALL_STORE_AUX>;
-  using Halves14 = StepCfg<kLut14Bits, true, false, false, false, MH_SMALL_STORE_AUX>;
-  using Halves13 = StepCfg<kLutBits, true, false, true, false, MH_SMALL_STORE_AUX>;
+  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux>;
+  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux>;
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
@@ -900,13 +762,10 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
     else
       decode_block<kDelta, Small13>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
   } else if (l14) {
-    decode_halves<kDelta, Halves14>(a, t, lane, lut, stage, out, row0, !t.valid);
+    decode_halves<kDelta, Small14>(a, t, lane, lut, stage, out, row0, !t.valid);
   } else {
-    decode_halves<kDelta, Halves13>(a, t, lane, lut, stage, out, row0, !t.valid);
+    decode_halves<kDelta, Small13>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
-#if MH_TLB_PREFETCH
-  if (warm == 0x9E3779B9u && lane == 64u) a.out[0] = 0;  // never true (lane < 64): keeps the loads
-#endif
 #if MH_DIAG_STAMPS
   MH_STAMP(4);
   ts[5] = ts[4];
@@ -932,10 +791,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 // masks through three ds_bpermutes on every step and stored every symbol to LDS
 // (35.7 vs 5.8 us); this one runs the default step with register output and swaps
 // the window masks only at sparse checkpoints.
-#ifndef MH_LP_WAVES
-#define MH_LP_WAVES 4
-#endif
-constexpr int kLpWaves = MH_LP_WAVES;
+constexpr int kLpWaves = 4;
 constexpr int kLpStageBytes = 4144;   // >= 15 + 32 blocks x 64 x 16 bits / 8 + 24, 16-B multiple
 static_assert(kLpStageBytes <= kStageChunks * 64 * 16, "span_issue covers the lane-pair stage");
 constexpr int kLpOutStride = 68;      // bytes per lane row (17 dwords: lanes spread over banks)
@@ -1226,12 +1082,12 @@ __global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const
   const uint32_t mid = t.p + (len >> 1);
   const uint32_t end = t.p + len;
   // the frame's last block has no exact end: lane A alone
-  const bool spec = t.valid && exact_end && len >= 2u * (uint32_t)MH_LP_MIN_BITS && len <= 64u * 16u;
+  const bool spec = t.valid && exact_end && len >= 2u * kLpMinBits && len <= 64u * 16u;
   if (l14)
-    lp_decode<kDelta, StepCfg<kLut14Bits, false>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
+    lp_decode<kDelta, StepCfg<kLut14Bits, false, false>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
                                                   spec, init, out, row0, (uint32_t)a.out_pitch);
   else
-    lp_decode<kDelta, StepCfg<kLutBits, false>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
+    lp_decode<kDelta, StepCfg<kLutBits, false, true>>(stage, lut, row_a, row_b, lane, t.valid, t.p, mid, end,
                                                 spec, init, out, row0, (uint32_t)a.out_pitch);
 }
 
@@ -1313,7 +1169,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
     MH_LAUNCH(mh_decode_lanepair_kernel<kDelta>, dim3(a.n_groups), dim3(kLpWaves * 64), s, any_order, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
-  if (MH_SMALL_KERNEL && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
+  if (a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // one tile per wave, kSmallWaves waves per workgroup: fewer workgroups copy the
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
     const uint32_t nw = kSmallWaves;
@@ -1326,15 +1182,8 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   uint32_t nw = (a.total_tiles + (uint32_t)cus - 1) / (uint32_t)cus;
   if (nw < 1) nw = 1;
   if (nw > (uint32_t)kMaxWavesPerWG) nw = kMaxWavesPerWG;
-#ifdef MH_FORCE_WAVES_PER_WG  // A/B: workgroup width for the config-3 balance study
-  if (a.total_tiles >= (uint32_t)(MH_FORCE_WAVES_PER_WG * cus)) nw = MH_FORCE_WAVES_PER_WG;
-#endif
   a.n_groups = (a.total_tiles + nw - 1) / nw;
-#ifdef MH_GRID_WGS_PER_CU  // A/B: cap the persistent grid below the occupancy limit
-  const uint32_t resident = (uint32_t)(cus * min(di->occ[kDelta ? 1 : 0][nw], MH_GRID_WGS_PER_CU));
-#else
   const uint32_t resident = (uint32_t)(cus * di->occ[kDelta ? 1 : 0][nw]);
-#endif
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
   MH_LAUNCH(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), s, any_order, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;

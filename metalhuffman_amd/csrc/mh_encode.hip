@@ -12,7 +12,7 @@
 //   block offsets    HuffmanUtil.cpp:1103-1128 -- an exclusive prefix sum of the
 //                    per-block code-length sums
 //   bit packing      HuffmanEncoder.cpp:211-381 -- MSB-first, staged per workgroup in LDS
-// Frames of <= MH_FUSED_MAX_TILES tiles: two launches, enc_split_kernel (tiled) and
+// Frames of <= kFusedMaxTiles tiles: two launches, enc_split_kernel (tiled) and
 // enc_code_kernel (workgroup 0 = tree, the others = offsets + packing of one tile each).
 // Larger frames: enc_split_kernel, enc_tree_kernel, enc_scan_kernel, enc_pack_kernel.
 // mh_encode_frame_device_async never synchronises (header, code bytes and status are
@@ -33,25 +33,17 @@ namespace {
 
 constexpr uint32_t kScanTile = 256;  // blocks per workgroup in the offsets scan
 constexpr uint32_t kResultBytes = 512;  // mh_encode_frame_device: header, byte count, status
-#ifndef MH_HIST_PARTS
-#define MH_HIST_PARTS 8
-#endif
-constexpr uint32_t kHistParts = MH_HIST_PARTS;  // partial histograms the split workgroups add into
-constexpr uint32_t kTicket = 16;        // meta[] slot of the offsets scan's completion counter
+constexpr uint32_t kHistParts = 8;      // partial histograms the split workgroups add into
 constexpr uint32_t kTotalBits = 17;     // meta[] slot of the frame's code bit count
 constexpr uint32_t kFlag = 18;          // meta[] slot: the code table is published (fused path)
 constexpr uint32_t kAbort = 19;         // meta[] slot: a packing workgroup gave up waiting (fused path)
-constexpr uint32_t kHistDone = 20;      // meta[] slot: tiles whose counts are in hist (one-launch path)
-constexpr uint32_t kDone = 21;          // meta[] slot: packing workgroups finished (one-launch path)
-constexpr uint32_t kGen = 22;           // meta[] slot: call generation of the fused paths (table tags, count tags)
+constexpr uint32_t kGen = 22;           // meta[] slot: call generation of the fused path (table tags)
 #ifndef MH_DIAG_SPIN_TICKS  // diagnostic builds only (tests/test_gpu_encode.py: forced timeout)
 #define MH_DIAG_SPIN_TICKS 10000000
 #endif
 constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;  // a packer's wait limit: 100 ms of s_memrealtime (100 MHz)
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
-#ifndef MH_FUSED_MAX_TILES              // frames up to this many tiles take the two-kernel path
-#define MH_FUSED_MAX_TILES 512
-#endif
+constexpr uint32_t kFusedMaxTiles = 512;  // frames up to this many tiles take the two-kernel path
 
 #ifndef MH_CODE_STAMPS  // diagnostic builds only: s_memrealtime phase stamps of enc_code_kernel
 #define MH_CODE_STAMPS 0
@@ -74,10 +66,8 @@ struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
   uint32_t *tsum;     // ceil(nb / kScanTile) tile sums (then tile offsets)
   uint64_t *hist;     // kHistParts x 256 partial counts
   uint32_t *table;    // 256 x (code_lj16 << 16 | len)
-  uint64_t *meta;     // [codes_len, ok flag, .., [kTicket] scan ticket, [kTotalBits], [kFlag]]
+  uint64_t *meta;     // [codes_len, ok flag, .., [kTotalBits], [kFlag], [kAbort], [kGen]]
   uint16_t *tile_hist;  // fused path: ceil(nb / kCodeTile) x 256 symbol counts
-  uint64_t *tstate;     // one-launch path: per code tile, look-back state (flag << 62 | bits)
-  uint32_t *claim;      // one-launch path: per code tile, who added its counts (1 itself, 2 the tree)
 };
 
 constexpr uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
@@ -95,18 +85,13 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   o += align256(kHistParts * 256 * 8);
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256(256 * 4);
-  // meta, tstate and claim are contiguous: the one-launch path's state, zeroed together
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
-  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
   o += align256((kGen + 1) * 8);
-  if (w) w->tstate = reinterpret_cast<uint64_t *>(base + o);
-  o += align256(ncode * 8);
-  if (w) w->claim = reinterpret_cast<uint32_t *>(base + o);
-  o += align256(ncode * 4);
-  // two-launch path: u16 counts per tile; one-launch path: u64 words of two
-  // generation-tagged u32 counts per tile (gen << 16 | count), so no zeroing per call
-  if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
-  o += align256(ncode * 256 * 4);
+  // hist, table and meta are contiguous: the per-call state a caller without
+  // MH_ENCODE_WORKSPACE_ZEROED gets zeroed by one memset (mh_encode_frame_device_async)
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);  // u16 counts per code tile
+  o += align256(ncode * 256 * 2);
   return o;
 }
 
@@ -117,20 +102,9 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
 // row up, histogram into 16 replicated LDS copies (BigBridge-like deltas are mostly
 // one symbol; one copy would serialise every atomic on it). Grid-stride over groups
 // of 32 blocks; one global atomic per used bin per workgroup.
-#ifndef MH_HIST_COPIES
-#define MH_HIST_COPIES 16
-#endif
-constexpr uint32_t kHistCopies = MH_HIST_COPIES;
-#ifndef MH_SPLIT_BATCH  // groups of 32 blocks whose rows a split workgroup loads at once
-#define MH_SPLIT_BATCH 8
-#endif
-constexpr uint32_t kSplitBatch = MH_SPLIT_BATCH;
-#ifndef MH_SPLIT_WGS  // split workgroups: each adds one global atomic per used bin
-#define MH_SPLIT_WGS 256
-#endif
-#ifndef MH_TREE_STAMPS
-#define MH_TREE_STAMPS 0
-#endif
+constexpr uint32_t kHistCopies = 16;
+constexpr uint32_t kSplitBatch = 8;   // groups of 32 blocks whose rows a split workgroup loads at once
+constexpr uint32_t kSplitWgs = 256;   // split workgroups (four-kernel path): one global atomic per used bin each
 
 // Row r (8 pixels, little-endian in a u64) of 8x8 block b, zero past the frame edge
 // (Util.m:256-318: zero-filled blocks, row-major inside a block).
@@ -169,17 +143,30 @@ __device__ __forceinline__ uint64_t row_symbols(uint64_t q, uint32_t r, bool del
   return v;
 }
 
-// Tiled mode (tile_hist != null, the fused path): workgroup t owns the kCodeTile
-// blocks of tile t (kCodeTile / 32 consecutive groups, loaded at once), stores the
-// tile's symbol counts in tile_hist[t] and re-arms the code kernel's table flag.
+// Tiled mode (tile_hist != null, the fused and batched paths): workgroup t owns the
+// kCodeTile blocks of tile t (kCodeTile / 32 consecutive groups, loaded at once) and
+// stores the tile's symbol counts in tile_hist[t]; with meta (the fused path) its
+// workgroup 0 re-arms the code kernel's table flag. Batched frames: workgroup
+// f * ncode + t is tile t of frame f (gray + f * gray_stride; per-frame block_init,
+// hist and tile_hist slices).
 constexpr uint32_t kTileGroups = kCodeTile / 32;
 static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgroup's batch covers a code tile");
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
                                                         uint32_t vec, uint8_t *sym, uint8_t *block_init,
-                                                        uint64_t *hist, uint16_t *tile_hist, uint64_t *meta) {
+                                                        uint64_t *hist, uint16_t *tile_hist, uint64_t *meta,
+                                                        uint32_t ncode, uint64_t gray_stride) {
   const bool tiled = tile_hist != nullptr;
-  if (tiled && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
+  uint32_t wg = blockIdx.x;  // tiled: this frame's tile
+  if (tiled) {
+    const uint32_t f = blockIdx.x / ncode;
+    wg = blockIdx.x - f * ncode;
+    gray += f * gray_stride;
+    if (block_init) block_init += (uint64_t)f * nb;
+    hist += (uint64_t)f * kHistParts * 256;
+    tile_hist += (uint64_t)f * ncode * 256;
+  }
+  if (tiled && meta && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
     meta[kFlag] = 0;
     meta[kAbort] = 0;
     meta[kGen] += 1;  // a new tag for the code table words (table_tag)
@@ -213,7 +200,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint64_t ngroups = (nb + 31) / 32;
   // grid-stride over groups, or (tiled) one batch of consecutive groups
   const uint64_t ustep = tiled ? 1u : gridDim.x;
-  const uint64_t gfirst = tiled ? (uint64_t)blockIdx.x * kTileGroups : blockIdx.x;
+  const uint64_t gfirst = tiled ? (uint64_t)wg * kTileGroups : blockIdx.x;
   const uint64_t gstride = tiled ? ngroups : (uint64_t)kSplitBatch * gridDim.x;
   for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
     const uint32_t nu = tiled ? kTileGroups : kSplitBatch;
@@ -234,23 +221,17 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   __syncthreads();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
-  if (tiled) tile_hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
+  if (tiled) tile_hist[(uint64_t)wg * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
   MH_SPLIT_STAMP(3)
   // kHistParts partial histograms (workgroups round-robin over them, as over the
   // XCDs): one address per bin would serialise every workgroup's atomic on it
-  if (c) atomicAdd((unsigned long long *)&hist[(blockIdx.x % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
+  if (c) atomicAdd((unsigned long long *)&hist[(wg % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
 #if MH_CODE_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   MH_SPLIT_STAMP(4)
 #endif
 }
 
-#ifndef MH_SCAN_TICKET   // 1: the scan's last workgroup (completion ticket) scans the tile totals;
-#define MH_SCAN_TICKET 0   // 0: each packing workgroup sums the totals before its own tile
-#endif
-#ifndef MH_TREE_BITONIC  // 1: each merge round orders the queue heads by a register bitonic merge
-#define MH_TREE_BITONIC 1
-#endif
 
 // Value of lane (lane ^ D) (64-lane wave): permlane32_swap for 32, ds_swizzle's xor
 // mode for 16 and 4, DPP (row rotate by 8, quad permutes) for 8, 2, 1.
@@ -289,15 +270,8 @@ __device__ __forceinline__ void bitonic_stage(uint32_t lane, uint64_t &key) {
 // one select on a lane-constant mask (no compare -> VCC -> select chain). The swap
 // stages (D = 32, 16) take min / max straight from the two permlane outputs: each lane
 // holds its own key in one and its partner's in the other.
-#ifndef MH_TREE_MINMAX
-#define MH_TREE_MINMAX 1
-#endif
-#ifndef MH_TREE_SORT_RANK  // 1: leaf ranks by wave bitonic sorts + binary search (32-bit keys)
-#define MH_TREE_SORT_RANK 1
-#endif
 template <uint32_t D>
 __device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
-#if MH_TREE_MINMAX
   uint32_t a, b;
   if constexpr (D == 32 || D == 16) {
     const auto r = D == 32 ? __builtin_amdgcn_permlane32_swap(key, key, false, false)
@@ -309,11 +283,6 @@ __device__ __forceinline__ void bitonic_stage32(uint32_t lane, uint32_t &key) {
     b = xor_partner<D>(lane, key);
   }
   key = (lane & D) ? max(a, b) : min(a, b);
-#else
-  const uint32_t p = xor_partner<D>(lane, key);
-  const bool take = (p < key) != ((lane & D) != 0u);  // keys are distinct
-  key = take ? p : key;
-#endif
 }
 
 // Ascending bitonic sort of one key per lane over the wave (21 compare-exchange stages
@@ -400,23 +369,16 @@ constexpr uint32_t kTreeThreads = 1024;  // 4 per symbol in the ranking; 256 (on
 // nsym: the frame's symbol count (64 per block). Below 2^22 - 1 every weight --
 // root included -- fits 22 bits, and the ranking and merge keys fit 32 bits.
 template <bool kFused>
-__device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta,
+// Returns, to the 256 symbol threads, symbol tid's table entry (code_lj16 << 16 | len;
+// 0 for an absent symbol) with bit 7 set when the frame is rejected; the other
+// threads return 0 early (before the symbol threads' last barriers).
+__device__ __forceinline__ uint32_t tree_body(uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta,
                                           uint64_t *codes_len_out, uint64_t codes_cap, int32_t *status,
                                           uint64_t nsym) {
   constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
   constexpr uint32_t kW32End = (1u << 22) - 1u;  // 32-bit merge keys: an empty slot's weight
   const bool k32 = nsym < (uint64_t)kW32End;
-#if MH_TREE_STAMPS  // phase timestamps (s_memtime) into meta[2..] for scripts/enc_profile.py
-#define MH_TREE_STAMP(k) \
-  if (tid == 0) meta[2 + (k)] = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) meta[2] = __builtin_amdgcn_s_memtime();
-#else
-#define MH_TREE_STAMP(k)
-#endif
   __shared__ uint32_t s_lw[384], s_iw[384];  // queues padded with kEnd
-#if !MH_TREE_BITONIC
-  __shared__ uint32_t s_qv[64], s_qid[64];
-#endif
   __shared__ __attribute__((aligned(16))) uint64_t s_key[256];
   __shared__ __attribute__((aligned(16))) uint32_t s_key32[256];
   __shared__ uint32_t s_leaf_sym[256], s_len[256], s_par[2][512], s_dep[2][512];
@@ -446,7 +408,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     s_total = 0;
   }
   __syncthreads();
-  MH_TREE_STAMP(1);
   {
     // rank of this leaf in (weight, symbol) order: count the smaller keys among all
     // 256 (16-byte broadcast reads, one 64-bit compare per key). Absent symbols
@@ -456,7 +417,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     const uint32_t ks = tid & 255u, part = tid >> 8;
     uint32_t below = 0, present;
     if (k32) {  // counts < 2^22: (count << 8 | symbol) fits 32 bits
-#if MH_TREE_SORT_RANK
       // The four symbol waves sort their 64 keys in registers (bitonic), then thread
       // (part, q) counts the keys of run `part` below sorted element q by binary search
       // (7 dependent LDS reads); q's rank is the sum over the four runs.
@@ -486,24 +446,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
           s_lw[rank] = k >> 8;
         }
       }
-#else
-      if (sym_thread) s_key32[tid] = f ? (uint32_t)(f << 8) | tid : 0u;
-      present = (uint32_t)__syncthreads_count(f != 0);
-      const uint32_t key = s_key32[ks];
-      const uint4 *kv = reinterpret_cast<const uint4 *>(s_key32) + part * 16u;
-#pragma unroll
-      for (uint32_t t = 0; t < 16; ++t) {  // same address across the wave: broadcast reads
-        const uint4 v = kv[t];
-        below += (v.x < key ? 1u : 0u) + (v.y < key ? 1u : 0u) + (v.z < key ? 1u : 0u) + (v.w < key ? 1u : 0u);
-      }
-      s_below[part][ks] = below;
-      __syncthreads();
-      if (sym_thread && f) {
-        const uint32_t rank = s_below[0][tid] + s_below[1][tid] + s_below[2][tid] + s_below[3][tid] - (256u - present);
-        s_leaf_sym[rank] = tid;
-        s_lw[rank] = (uint32_t)f;
-      }
-#endif
     } else {
       if (sym_thread) s_key[tid] = f ? (f << 8) | tid : 0;
       present = (uint32_t)__syncthreads_count(f != 0);
@@ -526,7 +468,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     if (tid == 0) s_n = present;
   }
   __syncthreads();
-  MH_TREE_STAMP(2);
   const uint32_t n = s_n;
   const uint32_t nodes = n ? 2 * n - 1 : 0, root = nodes - 1;
   if (n >= 2 && tid < 64) {
@@ -545,7 +486,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     const uint32_t lane = tid;
     uint32_t li = 0, ii = 0, ni = 0, m = 0;
     while (m + 1 < n) {
-#if MH_TREE_BITONIC
       // Q[0..63] by a bitonic merge in registers: key = weight : type : queue
       // position (a leaf sorts before an internal node of equal weight; each queue
       // keeps its order). min(A[i], B[63 - i]) holds the 64 smallest of both heads as
@@ -577,26 +517,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
         const uint32_t kl = (uint32_t)key;
         qid = (kl & 0x10000u) ? n + (kl & 0xFFFFu) : kl;
       }
-#else
-      const uint32_t lv = s_lw[li + lane], iv = s_iw[ii + lane];
-      uint32_t rl = 0, ri = 0;  // internal candidates < lv; leaf candidates <= iv
-#pragma unroll
-      for (uint32_t step = 64; step; step >>= 1) {
-        if (s_iw[ii + rl + step - 1] < lv) rl += step;
-        if (s_lw[li + ri + step - 1] <= iv) ri += step;
-      }
-      const uint32_t pl = lane + rl, pi = lane + ri;  // positions in Q
-      if (pl < 64) {
-        s_qv[pl] = lv;
-        s_qid[pl] = li + lane;
-      }
-      if (pi < 64) {
-        s_qv[pi] = iv;
-        s_qid[pi] = n + ii + lane;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t q = s_qv[lane], qid = s_qid[lane];
-#endif
       const uint32_t s0 = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_readlane(q, 1);
       // ballots of plain compares, masked on the scalar side (a ballot of a combined
       // condition re-materialises it in a VGPR first)
@@ -604,7 +524,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
       k = min(k, n - 1 - m);
       const uint64_t first2k = 2 * k >= 64 ? ~0ull : (1ull << (2 * k)) - 1ull;
       const uint32_t nl = (uint32_t)__popcll(__ballot(qid < n) & first2k);
-#if MH_TREE_BITONIC
       // pair j = lanes (2j, 2j+1): the odd lane adds its even neighbour (DPP) and
       // appends the new node; both lanes point their node at it
       const uint32_t qe = xor_partner<1>(lane, q);
@@ -612,15 +531,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
         if (lane & 1u) s_iw[ni + (lane >> 1)] = qe + q;
         s_par[0][qid] = n + ni + (lane >> 1);
       }
-#else
-      const uint32_t qa = __shfl(q, 2 * lane), qb = __shfl(q, 2 * lane + 1);
-      const uint32_t ia = __shfl(qid, 2 * lane), ib = __shfl(qid, 2 * lane + 1);
-      if (lane < k) {
-        s_iw[ni + lane] = qa + qb;
-        s_par[0][ia] = n + ni + lane;
-        s_par[0][ib] = n + ni + lane;
-      }
-#endif
       __builtin_amdgcn_wave_barrier();
       li += nl;
       ii += 2 * k - nl;
@@ -629,14 +539,12 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     }
   }
   __syncthreads();
-  MH_TREE_STAMP(3);
   // depths by pointer jumping: dep = 1 + dep(parent) over parent links, root 0
   for (uint32_t i = tid; i < nodes; i += kTreeThreads) {
     s_dep[0][i] = i == root ? 0u : 1u;
     if (i == root) s_par[0][i] = root;
   }
   __syncthreads();
-  MH_TREE_STAMP(4);
   // 4 rounds: a node within 16 hops of the root gets its exact depth and the root as
   // its ancestor; any other is deeper than 16 (MH_ERR_CODE_TOO_LONG)
   uint32_t cur = 0;
@@ -651,7 +559,7 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   }
   // the rest needs one thread per symbol: the other 12 waves end here (a finished
   // wave no longer counts at the workgroup barriers below)
-  if (!sym_thread) return;
+  if (!sym_thread) return 0u;
   if (n == 0) {
     if (tid == 0) s_bad = (uint32_t)-MH_ERR_EMPTY;
   } else if (n == 1) {  // single symbol -> 1-bit code "0" (HuffmanEncoder.cpp:118-121)
@@ -662,7 +570,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     s_len[s_leaf_sym[tid]] = d;
   }
   __syncthreads();
-  MH_TREE_STAMP(5);
   const uint32_t L = sym_thread ? s_len[tid] : 0u;  // 0 matches no length below
   if (sym_thread) canon_out[tid] = (uint8_t)L;
   // codes per length and each symbol's rank among equal lengths (symbol order):
@@ -679,7 +586,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
   for (int o = 32; o; o >>= 1) bits += __shfl_xor(bits, o);
   if (lane == 0 && wave < 4u) atomicAdd(&s_total, (unsigned long long)bits);
   __syncthreads();
-  MH_TREE_STAMP(6);
   if (tid < 64) {
     // first code of each length, the recurrence code = (code + count) << 1 in closed
     // form: first[l] = sum over j < l of count[j] << (l - j), a 16-lane prefix sum of
@@ -696,7 +602,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     if (tid < 16) s_first[ln] = (incl - v) >> (16 - ln);
   }
   __syncthreads();
-  MH_TREE_STAMP(7);
   uint32_t e = 0;
   if (L && L <= 16) {
     uint32_t rank = in_wave;  // symbols of the same length before this one
@@ -731,7 +636,6 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
     const uint64_t len = s_len_bytes;
     meta[0] = bad ? 0 : len;
     meta[1] = bad ? 0 : 1;
-    meta[kTicket] = 0;
     meta[kTotalBits] = s_total;
     if (codes_len_out) *codes_len_out = bad ? 0 : len;
     if (status) {
@@ -748,7 +652,8 @@ __device__ __forceinline__ void tree_body(uint64_t *hist, uint8_t *canon_out, ui
       }
     }
   }
-  MH_TREE_STAMP(8);
+  if constexpr (!kFused) __syncthreads();  // s_bad2 (the fused path had its barrier above)
+  return e | (s_bad2 ? 0x80u : 0u);
 }
 
 __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, uint8_t *canon_out,
@@ -760,9 +665,8 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_kernel(uint64_t *hist, 
 // Block offsets, one kernel: each workgroup zeroes its share of the code words the
 // packing ORs into (round_up(codes_len, 4) bytes, sized on the device), sums the
 // code lengths of kScanTile blocks (HuffmanUtil.cpp:1103-1128 counts bits per block
-// the same way), scans them in place and records the tile total; the last
-// workgroup to finish (a ticket in meta[kTicket], reset by enc_tree_kernel) turns
-// the tile totals into tile offsets.
+// the same way), scans them in place and records the tile total; each packing
+// workgroup sums the totals of the tiles before its own (enc_pack_kernel).
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
   const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
@@ -798,7 +702,6 @@ __global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym,
                                                              uint64_t *meta, uint32_t *words) {
   __shared__ uint32_t len[256];
   __shared__ uint32_t s_w[kScanTile / 64];
-  __shared__ uint32_t last;
   const uint32_t tid = threadIdx.x;
   if (tid < 256) len[tid] = table[tid] & 0xFFu;
   const uint64_t nw = meta[1] ? (meta[0] + 3) / 4 : 0;
@@ -819,37 +722,8 @@ __global__ void __launch_bounds__(kScanTile) enc_scan_kernel(const uint8_t *sym,
   uint32_t total;
   const uint32_t pre = wg_exclusive_scan(x, s_w, &total);
   if (i < nb) bpre[i] = pre;
-#if !MH_SCAN_TICKET
   // tile totals only: each packing workgroup sums the totals before its tile
   if (tid == 0) tsum[blockIdx.x] = total;
-  (void)last;
-  return;
-#endif
-  if (tid == 0) {
-    // The tile total goes out as a device-scope store (written through past this
-    // XCD's L2) and is acknowledged before the ticket is taken, so the last
-    // workgroup's device-scope loads see every total. A __threadfence() here would
-    // write back this XCD's whole L2 (buffer_wbl2) in every workgroup: 1 us more.
-    __hip_atomic_store(&tsum[blockIdx.x], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kTicket]), 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1
-               ? 1u
-               : 0u;
-  }
-  __syncthreads();
-  if (!last) return;
-  const uint64_t ntiles = gridDim.x;
-  uint32_t carry = 0;
-  for (uint64_t base = 0; base < ntiles; base += kScanTile) {
-    const uint64_t t = base + tid;
-    // other workgroups' totals: device-coherent loads (past this CU's L1)
-    const uint32_t v = t < ntiles ? __hip_atomic_load(&tsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    uint32_t chunk;
-    const uint32_t p = wg_exclusive_scan(v, s_w, &chunk);
-    if (t < ntiles) tsum[t] = carry + p;
-    carry += chunk;
-  }
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
@@ -877,16 +751,6 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
   const uint64_t b0 = (uint64_t)blockIdx.x * kPackBlocks, b = b0 + (tid >> 3);
   const bool on = b < nb;
   const uint64_t q = on ? reinterpret_cast<const uint64_t *>(sym + b * 64)[part] : 0ull;
-#if MH_SCAN_TICKET
-  const uint32_t o = on ? blen_prefix[b] + toff[b / kScanTile] : 0u;
-  if (on && part == 0) offsets[b] = o;
-  if (tid == 0) {
-    const uint64_t bn = b0 + kPackBlocks;
-    s_start = o;
-    s_end = bn < nb ? blen_prefix[bn] + toff[bn / kScanTile] : (uint32_t)meta[kTotalBits];
-  }
-  __syncthreads();
-#else
   // this workgroup's tile offset: wave 0 sums the scan's tile totals before it
   // (<= a few hundred L2-resident words) -- no completion ticket in the scan
   __shared__ uint32_t s_toff[2];
@@ -909,7 +773,6 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
     s_end = bn < nb ? blen_prefix[bn] + s_toff[bn / kScanTile == t ? 0 : 1] : (uint32_t)meta[kTotalBits];
   }
   __syncthreads();
-#endif
   const uint32_t w0 = s_start >> 5, nwords = ((s_end + 31) >> 5) - w0;
   for (uint32_t i = tid; i < nwords; i += 256) lw[i] = 0;
   uint32_t e[8], nbits = 0;
@@ -976,9 +839,7 @@ __global__ void __launch_bounds__(256) enc_pack_kernel(const uint8_t *sym, const
 // next tile (the last tile writes it and the zero pad). Every code word is written
 // exactly once, so the buffer needs no clearing.
 constexpr uint32_t kCodeThreads = 1024;
-#ifndef MH_CODE_MIN_WAVES  // waves per SIMD the register budget must admit (A/B)
-#define MH_CODE_MIN_WAVES 8
-#endif
+constexpr uint32_t kCodeMinWaves = 8;  // waves per SIMD the register budget must admit
 constexpr uint32_t kCodeWaves = kCodeThreads / 64;
 constexpr uint32_t kCodeWords = kCodeTile * 64 * 16 / 32 + 2;  // a tile's code words, <= 16-bit codes
 static_assert(kCodeThreads == 8 * kCodeTile, "eight lanes per block");
@@ -1011,13 +872,95 @@ struct Pixels {  // the frame as the split reads it
   bool delta, init_byte;
 };
 
+// Tile t's code words once its first bit E is known (tab = the frame's code table in
+// LDS, q = this lane's eight symbols, qp = lanes 0-7 of wave 0: the previous block's
+// row symbols). Block offsets out; a tile's first word shares bits with the previous
+// tile's last block (every block has >= 64 bits, a word holds 32): the workgroup
+// computes those bits itself from that block's symbols and writes the word whole; a
+// tile leaves its own partial last word to the next tile (the last tile writes it and
+// the zero pad). Every code word is written exactly once: no clearing, no atomics.
+__device__ __forceinline__ void pack_emit(uint32_t t, uint32_t ntiles, uint32_t E, const uint32_t *tab,
+                                          uint64_t q, uint64_t qp, uint64_t b, bool on, uint32_t *offsets,
+                                          uint32_t *words) {
+  __shared__ uint32_t lw[kCodeWords];
+  __shared__ uint32_t s_scan[kCodeWaves];
+  const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
+  (void)part;
+  // this lane's codes, as two chunks of four (<= 64 bits each)
+  uint64_t ch[2] = {0, 0};
+  uint32_t cl[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t e = tab[(uint32_t)(q >> (8 * j)) & 0xFFu];
+    const uint32_t len = e & 0xFFu;
+    ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
+    cl[j >> 2] += len;
+  }
+  const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
+  // exclusive scan over the 1024 lanes (lane order = block order, eight lanes each)
+  const uint32_t incl = wave_scan_dpp(nbits);
+  if (lane == 63) s_scan[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
+    if (lane < kCodeWaves) s_scan[lane] = v;
+  }
+  __syncthreads();
+  const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
+  const uint32_t T = s_scan[kCodeWaves - 1];
+  MH_CODE_STAMP(t + 1, 4)
+  if (on && part == 0) offsets[b] = E + pre;
+  const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
+  const uint32_t nwords = ((end + 31u) >> 5) - w0;
+  for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
+  // the previous block's last r bits, the head of this tile's first word (lanes 0-7)
+  uint32_t head = 0;
+  if (r && wave == 0) {
+    uint32_t lenp = 0;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
+      const uint32_t len = e & 0xFFu;
+      // the lane's codes MSB-first; keep the last 64 bits (r <= 31 of them are used)
+      acc = (acc << len) | ((e >> 16) >> (16 - len));
+      lenp += len;
+    }
+    if (lane >= 8) lenp = 0;
+    // bits of lanes after this one (in block order) = suffix sum over lanes 0-7
+    const uint32_t incp = wave_scan_dpp(lenp);
+    const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
+    // the word's first r bits are the block's last r bits; this lane's code bits end
+    // `after` bits before the block's end, so its last bit is word bit 32 - r + after
+    // (bits that would land before the word fall off the top)
+    if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
+    for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
+  }
+  __syncthreads();
+  if (on) {
+    or_bits(lw, r + pre, ch[0], cl[0]);
+    or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
+  }
+  if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
+  __syncthreads();
+  MH_CODE_STAMP(t + 1, 5)
+  // a partial last word belongs to the next tile (it adds its own first bits); the
+  // last tile writes it, then the zero pad up to the byte count rounded to words
+  const bool last = t + 1 == ntiles;
+  const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
+  for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
+  if (last) {
+    const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
+    for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
+  }
+}
+
 __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uint16_t *tile_hist,
                                           const uint32_t *table, uint64_t *meta, uint64_t nb, uint32_t ntiles,
                                           uint32_t *offsets, uint32_t *words, int32_t *status) {
   __shared__ uint32_t tab[256];
-  __shared__ uint32_t lw[kCodeWords];
   __shared__ uint32_t s_cnt[kCodeWaves][256];  // symbol counts of the tiles before this one, per wave
-  __shared__ uint32_t s_dot[4], s_scan[kCodeWaves];
+  __shared__ uint32_t s_dot[4];
   const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
   MH_CODE_STAMP(t + 1, 0)
   const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
@@ -1032,11 +975,7 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
     // 32nd tile, eight loads in flight per lane (a late tile sums ~400 rows);
     // lanes l and l + 32 hold the same bins, the 16 waves' partials meet in LDS
     const uint32_t q4 = tid & 31u, j = tid >> 5;
-#ifdef MH_DIAG_CODE_NOHIST  // timing diagnostics only (wrong output)
-    const uint32_t tlim = 0;
-#else
     const uint32_t tlim = t;
-#endif
     const uint4 *th = reinterpret_cast<const uint4 *>(tile_hist);
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t u0 = j; u0 < tlim; u0 += 32u * 8u) {
@@ -1085,74 +1024,9 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
     const uint32_t x = wave_scan_dpp(c * (tab[tid] & 0xFFu));
     if (lane == 63) s_dot[wave] = x;
   }
-  // this lane's codes, as two chunks of four (<= 64 bits each)
-  uint64_t ch[2] = {0, 0};
-  uint32_t cl[2] = {0, 0};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t e = tab[(uint32_t)(q >> (8 * j)) & 0xFFu];
-    const uint32_t len = e & 0xFFu;
-    ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
-    cl[j >> 2] += len;
-  }
-  const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
-  // exclusive scan over the 1024 lanes (lane order = block order, eight lanes each)
-  const uint32_t incl = wave_scan_dpp(nbits);
-  if (lane == 63) s_scan[wave] = incl;
-  __syncthreads();
-  if (wave == 0) {
-    const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
-    if (lane < kCodeWaves) s_scan[lane] = v;
-  }
   __syncthreads();
   const uint32_t E = s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
-  const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
-  const uint32_t T = s_scan[kCodeWaves - 1];
-  MH_CODE_STAMP(t + 1, 4)
-  if (on && part == 0) offsets[b] = E + pre;
-  const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
-  const uint32_t nwords = ((end + 31u) >> 5) - w0;
-  for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
-  // the previous block's last r bits, the head of this tile's first word (lanes 0-7)
-  uint32_t head = 0;
-  if (r && wave == 0) {
-    uint32_t lenp = 0;
-    uint64_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
-      const uint32_t len = e & 0xFFu;
-      // the lane's codes MSB-first; keep the last 64 bits (r <= 31 of them are used)
-      acc = (acc << len) | ((e >> 16) >> (16 - len));
-      lenp += len;
-    }
-    if (lane >= 8) lenp = 0;
-    // bits of lanes after this one (in block order) = suffix sum over lanes 0-7
-    const uint32_t incp = wave_scan_dpp(lenp);
-    const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
-    // the word's first r bits are the block's last r bits; this lane's code bits end
-    // `after` bits before the block's end, so its last bit is word bit 32 - r + after
-    // (bits that would land before the word fall off the top)
-    if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
-    for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
-  }
-  __syncthreads();
-  if (on) {
-    or_bits(lw, r + pre, ch[0], cl[0]);
-    or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
-  }
-  if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
-  __syncthreads();
-  MH_CODE_STAMP(t + 1, 5)
-  // a partial last word belongs to the next tile (it adds its own first bits); the
-  // last tile writes it, then the zero pad up to the byte count rounded to words
-  const bool last = t + 1 == ntiles;
-  const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
-  for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
-  if (last) {
-    const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
-    for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
-  }
+  pack_emit(t, ntiles, E, tab, q, qp, b, on, offsets, words);
 #if MH_CODE_STAMPS
   if (tid == 0 && t + 1 < kCodeStampWgs)
     g_code_stamps[(t + 1) * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
@@ -1163,16 +1037,13 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
 #endif
 }
 
-__global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kernel(uint64_t *hist, uint8_t *canon_out, uint32_t *table,
+__global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_code_kernel(uint64_t *hist, uint8_t *canon_out, uint32_t *table,
                                                                 uint64_t *meta, uint64_t *codes_len_out,
                                                                 uint64_t codes_cap, int32_t *status,
                                                                 const Pixels px, const uint16_t *tile_hist,
                                                                 uint64_t nb, uint32_t ntiles, uint32_t *offsets,
                                                                 uint32_t *words) {
   static_assert(kTreeThreads == kCodeThreads, "workgroup 0 runs the tree");
-#ifdef MH_DIAG_CODE_NOPACK  // timing diagnostics only (wrong output)
-  if (blockIdx.x != 0) return;
-#endif
   if (blockIdx.x == 0) {
     MH_CODE_STAMP(0, 0)
     tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
@@ -1182,395 +1053,131 @@ __global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_code_kern
   pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, status);
 }
 
-// ---- the one-launch path: enc_one_kernel ------------------------------------------
-// One launch for frames of <= MH_FUSED_MAX_TILES code tiles, each pixel read once.
-// Workgroup t + 1 loads tile t's pixels (kept in registers), derives the symbols, counts
-// them in LDS and publishes the counts as generation-tagged words; workgroup 0 sums every
-// tile's words (a tile whose workgroup has not started after a bounded wait is claimed
-// and counted by workgroup 0 itself, so the launch cannot deadlock however few
-// workgroups are resident), builds the tree (tree_body<true>) and publishes the code
-// table. Each packing workgroup then takes its own tile's bit count (its counts x code
-// lengths), publishes it, and sums every earlier tile's count in one round of loads for
-// its first bit -- instead of re-reading every earlier tile's histogram (the two-launch
-// path) or walking a look-back chain. The last workgroup to finish re-zeroes the launch
-// state and bumps the generation for the next frame.
-constexpr uint64_t kAggFlag = 1ull << 62, kValMask = (1ull << 62) - 1ull;
-#ifndef MH_ONE_CLAIM_TICKS  // workgroup 0's wait before it counts missing tiles itself (s_memrealtime, 100 MHz)
-#define MH_ONE_CLAIM_TICKS 2000  // 20 us
-#endif
+// ---- batched frames: enc_split_kernel (tiled) + enc_tree_batch_kernel + enc_pack_batch_kernel
+// N independent frames of one size, each with its own histogram, tree and code table,
+// in three launches whatever N (mh_encode_frames_device_async). The kernel boundaries
+// order the phases, so no workgroup waits on another: the split (N x tiles workgroups)
+// writes per-tile symbol counts; workgroup f of the tree kernel builds frame f's tree
+// (tree_body) and then the frame's tile offsets (each tile's bits = its counts x the
+// code lengths, exclusive scan); the pack kernel (N x tiles workgroups) turns each
+// tile into code words from its first bit. Frames no longer queue behind one
+// workgroup's ~10 us tree each (the single-frame path): the N trees run side by side.
+constexpr uint32_t kMetaWords = 32;  // per-frame meta slots (>= kGen + 1)
+static_assert(kMetaWords >= kGen + 1, "meta slots");
+constexpr uint32_t kTileBatch = 32;  // tiles per wave and chunk of the tile-offset pass
 
-// Counts of tile t's symbols into h (256 x kHistCopies words of LDS, zeroed) by all
-// kCodeThreads threads; returns this lane's symbols (q) and its row pixels' block.
-__device__ __forceinline__ uint64_t tile_symbols(const Pixels px, uint64_t nb, uint32_t t, uint32_t *h,
-                                                 uint32_t *first) {
-  const uint32_t tid = threadIdx.x, part = tid & 7u;
-  const uint64_t b = (uint64_t)t * kCodeTile + (tid >> 3);
-  const uint64_t g = block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b, part);
-  const uint64_t q = row_symbols(g, part, px.delta, px.init_byte, first);
-  if (b < nb) {
-    const uint32_t copy = tid % kHistCopies;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(q >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+__global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
+    uint64_t *hist, uint8_t *canon, uint32_t *table, uint64_t *meta, uint64_t *codes_len, uint64_t codes_cap,
+    int32_t *status, uint64_t nb, const uint16_t *tile_hist, uint32_t ncode, uint32_t *tile_off,
+    uint64_t *frame_off, uint32_t n_frames) {
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  if (frame_off && tid == 0) {  // optional: the decoder's frame_code_offsets for fixed slots
+    frame_off[f] = (uint64_t)f * codes_cap;
+    if (f + 1 == n_frames) frame_off[n_frames] = (uint64_t)n_frames * codes_cap;
   }
-  return q;
-}
-
-__device__ __forceinline__ uint32_t call_gen(const uint64_t *meta) {
-  return (__hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kGen]), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT) % 65535u) + 1u;
-}
-
-// Workgroup 0, before the tree: the frame's 256 symbol counts into hist (part 0).
-// Each packing workgroup publishes its tile's counts as 128 u64 words of two tagged
-// counts (gen << 16 | count), one relaxed atomic store each: a word is valid when its
-// tags equal this call's generation, so there is no flag to order and no release (a
-// release fence writes the XCD's whole L2 back) and nothing to zero between calls.
-// Workgroup 0 first waits (bounded) on a published-tiles hint counter; tiles whose
-// workgroups have not claimed them by then are claimed and counted here (the launch
-// cannot deadlock however few workgroups are resident); then it sums every other
-// tile's words, 8 loads in flight per thread, waiting on any word not yet valid.
-__device__ __forceinline__ void wait_histograms(const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *hist,
-                                                uint64_t *meta, uint32_t *claim, const uint64_t *thw,
-                                                uint32_t *h) {
-  __shared__ uint32_t s_done, s_mine, s_list[MH_FUSED_MAX_TILES], s_own[256];
-  __shared__ uint32_t s_mask[(MH_FUSED_MAX_TILES + 31) / 32];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t gen = call_gen(meta);
-  if (tid < 256) s_own[tid] = 0;
-  if (tid < (MH_FUSED_MAX_TILES + 31) / 32) s_mask[tid] = 0;
-  if (tid == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t d;
-    while ((d = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&meta[kHistDone]), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT)) < ntiles &&
-           __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)MH_ONE_CLAIM_TICKS)
-      __builtin_amdgcn_s_sleep(2);
-    s_done = d >= ntiles ? 1u : 0u;
-    s_mine = 0;
-    MH_CODE_STAMP(0, 3)
-  }
+  const uint32_t e = tree_body<false>(hist + (uint64_t)f * kHistParts * 256, canon + (uint64_t)f * 256,
+                                      table + (uint64_t)f * 256, meta + (uint64_t)f * kMetaWords,
+                                      codes_len ? codes_len + f : nullptr, codes_cap, status ? status + f : nullptr,
+                                      nb * 64);
+  if (tid >= 256) return;  // tree_body leaves the 256 symbol threads (4 waves)
+  __shared__ uint32_t s_len[256], s_chunk[4 * kTileBatch];
+  s_len[tid] = e & 0x1Fu;
   __syncthreads();
-  if (!s_done) {
-    // Rare: wave 0 tries to claim every unclaimed tile (64 claims at once); the packer
-    // that starts later finds its claim taken and publishes nothing. The whole
-    // workgroup counts the claimed tiles into s_own.
-    if (tid < 64) {
-      uint32_t k = 0;  // tiles claimed so far (the same in every lane)
-      for (uint32_t base = 0; base < ntiles; base += 64) {
-        const uint32_t t = base + lane;
-        bool got = false;
-        if (t < ntiles && __hip_atomic_load(&claim[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          uint32_t z = 0;
-          got = __hip_atomic_compare_exchange_strong(&claim[t], &z, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const uint64_t m = __ballot(got);
-        if (got) {
-          s_list[k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = t;
-          atomicOr(&s_mask[t >> 5], 1u << (t & 31u));
-        }
-        k += (uint32_t)__popcll(m);
-      }
-      if (lane == 0) s_mine = k;
+  if (e & 0x80u) return;  // rejected frame (uniform): the pack kernel writes nothing
+  // Tile offsets: wave w reduces tiles c + w * kTileBatch + [0, kTileBatch) of each chunk
+  // of 4 * kTileBatch tiles (lane l: symbols 4l..4l+3 of a tile, one 8-byte load; all
+  // kTileBatch loads in flight); wave 0 scans the chunk's totals with a running carry.
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  const uint2 *th = reinterpret_cast<const uint2 *>(tile_hist + (uint64_t)f * ncode * 256);
+  uint32_t *to = tile_off + (uint64_t)f * (ncode + 1);
+  const uint32_t l0 = s_len[4 * lane], l1 = s_len[4 * lane + 1], l2 = s_len[4 * lane + 2], l3 = s_len[4 * lane + 3];
+  uint32_t carry = 0;
+  for (uint32_t c = 0; c < ncode; c += 4 * kTileBatch) {
+    const uint32_t t0 = c + wave * kTileBatch;
+    uint2 v[kTileBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kTileBatch; ++k)
+      v[k] = t0 + k < ncode ? th[(uint64_t)(t0 + k) * 64 + lane] : make_uint2(0u, 0u);
+#pragma unroll
+    for (uint32_t k = 0; k < kTileBatch; ++k) {
+      uint32_t x = (v[k].x & 0xFFFFu) * l0 + (v[k].x >> 16) * l1 + (v[k].y & 0xFFFFu) * l2 + (v[k].y >> 16) * l3;
+      x = wave_scan_dpp(x);
+      if (lane == 63) s_chunk[wave * kTileBatch + k] = x;  // the tile's bits (< 2^21)
     }
     __syncthreads();
-    const uint32_t mine = s_mine;
-    for (uint32_t i = 0; i < mine; ++i) {
-      const uint32_t t = s_list[i];
-      for (uint32_t j = tid; j < 256 * kHistCopies; j += kCodeThreads) h[j] = 0;
-      __syncthreads();
-      uint32_t first_unused;
-      tile_symbols(px, nb, t, h, &first_unused);
-      __syncthreads();
-      if (tid < 256) {
-        uint32_t c = 0;
-        for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
-        s_own[tid] += c;
-      }
-      __syncthreads();
+    if (wave == 0) {
+      // 4 * kTileBatch = 128 totals: two per lane
+      const uint32_t a = s_chunk[2 * lane], b = s_chunk[2 * lane + 1];
+      const uint32_t incl = wave_scan_dpp(a + b);
+      const uint32_t base = carry + incl - (a + b);
+      if (c + 2 * lane < ncode) to[c + 2 * lane] = base;
+      if (c + 2 * lane + 1 < ncode) to[c + 2 * lane + 1] = base + a;
+      carry += __builtin_amdgcn_readlane(incl, 63);
     }
-  }
-  // every tile not counted here: its words, once tagged with this generation
-  {
-    const uint32_t col = tid & 127u, grp = tid >> 7;  // bins 2col, 2col+1; tiles grp, grp + 8, ...
-    const uint32_t tag = gen << 16;
-    uint32_t c0 = 0, c1 = 0;
-    for (uint32_t t0 = grp; t0 < ntiles; t0 += 8u * 8u) {
-      uint64_t v[8];
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t t = t0 + 8u * k;
-        v[k] = t < ntiles ? __hip_atomic_load(&thw[(uint64_t)t * 128 + col], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
-                          : 0ull;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t t = t0 + 8u * k;
-        if (t >= ntiles || ((s_mask[t >> 5] >> (t & 31u)) & 1u)) continue;
-        uint64_t x = v[k];
-        while (((uint32_t)x & 0xFFFF0000u) != tag || ((uint32_t)(x >> 32) & 0xFFFF0000u) != tag) {
-          __builtin_amdgcn_s_sleep(1);
-          x = __hip_atomic_load(&thw[(uint64_t)t * 128 + col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        c0 += (uint32_t)x & 0xFFFFu;
-        c1 += (uint32_t)(x >> 32) & 0xFFFFu;
-      }
-    }
-    __syncthreads();  // h is free again
-    MH_CODE_STAMP(0, 4)
-    h[grp * 256 + 2 * col] = c0;
-    h[grp * 256 + 2 * col + 1] = c1;
     __syncthreads();
-    if (tid < 256) {
-      uint64_t f = s_own[tid];
-#pragma unroll
-      for (uint32_t g = 0; g < 8; ++g) f += h[g * 256 + tid];
-      hist[tid] = f;  // part 0; the tree reads (and re-zeroes) every part
-    }
-    // words of tiles counted here stay stale: clear them so a later generation with the
-    // same tag (65535 calls on) cannot mistake them
-    if (s_mine)
-      for (uint32_t i = 0; i < s_mine; ++i)
-        if (tid < 128) __hip_atomic_store((uint64_t *)&thw[(uint64_t)s_list[i] * 128 + tid], 0ull, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();
+  if (tid == 0) to[ncode] = carry;
 }
 
-// The last workgroup of the launch to get here (the ntiles packers and workgroup 0, once
-// its table is out) re-zeroes the launch state for the next frame: by then no look-back,
-// claim or histogram wait can still read it. `nthreads` threads of the workgroup call it.
-__device__ __forceinline__ void finish_launch(uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint32_t ntiles,
-                                              uint32_t nthreads) {
-  __shared__ uint32_t s_last;
-  const uint32_t tid = threadIdx.x;
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t done = __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kDone]), 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    s_last = done == ntiles ? 1u : 0u;  // ntiles + 1 participants
-  }
-  __syncthreads();
-  if (!s_last) return;
-  for (uint32_t i = tid; i < ntiles; i += nthreads) {
-    __hip_atomic_store(&tstate[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&claim[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tid == 0) {
-    for (uint32_t k : {kHistDone, kFlag, kAbort, kDone})
-      __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[k]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kGen]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ __forceinline__ void pack_tile_one(uint32_t t, const Pixels px, uint64_t *hist, const uint32_t *table,
-                                              uint64_t *meta, uint64_t *tstate, uint32_t *claim, uint64_t nb,
-                                              uint32_t ntiles, uint32_t *offsets, uint32_t *words, int32_t *status,
-                                              uint32_t *h, uint8_t *block_init, uint64_t *thw) {
+__global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_pack_batch_kernel(
+    const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
+    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride) {
   __shared__ uint32_t tab[256];
-  __shared__ uint32_t lw[kCodeWords];
-  __shared__ uint32_t s_cnt[256];
-  __shared__ uint32_t s_dot[4], s_scan[kCodeWaves];
-  __shared__ uint32_t s_flag, s_E;
-  const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t f = blockIdx.x / ncode, t = blockIdx.x - f * ncode;
+  if (!meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (status set by the tree)
+  const uint32_t tid = threadIdx.x, part = tid & 7u;
+  const uint8_t *gray = px.gray + f * gray_stride;
   const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
   const bool on = b < nb;
-  MH_CODE_STAMP(t + 1, 0)
-  bool claimed = false;
-  if (tid == 0) {  // this tile's counts are published unless workgroup 0 took the tile over
-    uint32_t z = 0;
-    claimed = __hip_atomic_compare_exchange_strong(&claim[t], &z, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (uint32_t i = tid; i < 256 * kHistCopies; i += kCodeThreads) h[i] = 0;
-  // (lanes 0-7, t > 0) the previous block's rows: the head bits of this tile's first word
-  const uint64_t gp = (t > 0 && tid < 8) ? block_row(px.gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
-  __syncthreads();
-  uint32_t first, first_unused;
-  const uint64_t q = tile_symbols(px, nb, t, h, &first);
-  if (block_init && part == 0 && on) block_init[b] = (uint8_t)first;  // AAPLRenderer.m:449-473
+  const uint64_t gq = block_row(gray, px.W, px.H, px.bw, nb, px.vec, b, part);
+  const uint64_t gp = (t > 0 && tid < 8) ? block_row(gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
+  if (tid < 256) tab[tid] = table[(uint64_t)f * 256 + tid];
+  const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
+  uint32_t first_unused;
+  const uint64_t q = row_symbols(gq, part, px.delta, px.init_byte, &first_unused);
   const uint64_t qp = row_symbols(gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // lanes 0-7 of wave 0
-  __syncthreads();
-  if (tid < 256) {
-    uint32_t c = 0;
-    for (uint32_t k = 0; k < kHistCopies; ++k) c += h[tid * kHistCopies + ((k + tid) % kHistCopies)];
-    s_cnt[tid] = c;
-  }
-  if (tid == 0) s_flag = claimed ? 1u : 0u;
-  __syncthreads();
-  const bool mine = s_flag != 0;
-  if (mine && tid < 128) {  // this tile's counts as tagged words (see wait_histograms)
-    const uint32_t tag = call_gen(meta) << 16;
-    const uint64_t w = (uint64_t)(tag | s_cnt[2 * tid]) | ((uint64_t)(tag | s_cnt[2 * tid + 1]) << 32);
-    __hip_atomic_store(&thw[(uint64_t)t * 128 + tid], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tid == 0) {
-    if (mine)  // a hint for workgroup 0's wait only: the words carry their own validity
-      __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&meta[kHistDone]), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    MH_CODE_STAMP(t + 1, 1)
-  }
-  const uint32_t f = wait_table(table, meta, tab, 16);  // tagged words: see tree_body
-  MH_CODE_STAMP(t + 1, 2)
-  if (f == 1u) {
-    // this tile's bit count: its counts x code lengths
-    if (wave < 4) {
-      const uint32_t x = wave_scan_dpp(s_cnt[tid] * (tab[tid] & 0xFFu));
-      if (lane == 63) s_dot[wave] = x;
-    }
-    // this lane's codes, as two chunks of four (<= 64 bits each)
-    uint64_t ch[2] = {0, 0};
-    uint32_t cl[2] = {0, 0};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t e = tab[(uint32_t)(q >> (8 * j)) & 0xFFu];
-      const uint32_t len = e & 0xFFu;
-      ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
-      cl[j >> 2] += len;
-    }
-    const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
-    const uint32_t incl = wave_scan_dpp(nbits);
-    if (lane == 63) s_scan[wave] = incl;
-    __syncthreads();
-    if (wave == 0) {
-      // This tile's first bit = the sum of every earlier tile's bit count. Each tile
-      // publishes its count (one 64-bit word, flag and value together, so relaxed
-      // atomics suffice) as soon as the table is out; wave 0 then reads all earlier
-      // counts at once (<= 8 loads in flight per lane: one round trip) -- no serial
-      // look-back chain. A tile that never publishes (its workgroup gave up) times out
-      // this one too.
-      const uint64_t agg = (uint64_t)s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
-      if (lane == 0)
-        __hip_atomic_store(&tstate[t], kAggFlag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint64_t v[MH_FUSED_MAX_TILES / 64];
-#pragma unroll
-      for (uint32_t k = 0; k < MH_FUSED_MAX_TILES / 64; ++k) {
-        const uint32_t u = lane + 64u * k;
-        v[k] = u < t ? __hip_atomic_load(&tstate[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kAggFlag;
-      }
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      bool lane_ok = true;
-      uint64_t x = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < MH_FUSED_MAX_TILES / 64; ++k) {
-        const uint32_t u = lane + 64u * k;
-        while (lane_ok && (v[k] >> 62) == 0u) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) lane_ok = false;
-          __builtin_amdgcn_s_sleep(1);
-          v[k] = __hip_atomic_load(&tstate[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        x += u < t ? (v[k] & kValMask) : 0ull;
-      }
-      for (uint32_t o = 32; o; o >>= 1) x += __shfl_xor(x, o);
-      const bool ok = __ballot(!lane_ok) == 0;
-      if (lane == 0) {
-        s_E = (uint32_t)x;
-        s_flag = ok ? 1u : 3u;
-      }
-      MH_CODE_STAMP(t + 1, 3)
-    }
-    __syncthreads();
-    if (wave == 0) {
-      const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
-      if (lane < kCodeWaves) s_scan[lane] = v;
-    }
-    __syncthreads();
-    if (s_flag != 1u) {
-      if (tid == 0) {
-        __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      goto finish;
-    }
-    {
-    const uint32_t E = s_E;
-    const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
-    const uint32_t T = s_scan[kCodeWaves - 1];
-    if (on && part == 0) offsets[b] = E + pre;
-    const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
-    const uint32_t nwords = ((end + 31u) >> 5) - w0;
-    for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
-    // the previous block's last r bits, the head of this tile's first word (lanes 0-7)
-    uint32_t head = 0;
-    if (r && wave == 0) {
-      uint32_t lenp = 0;
-      uint64_t acc = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
-        const uint32_t len = e & 0xFFu;
-        acc = (acc << len) | ((e >> 16) >> (16 - len));
-        lenp += len;
-      }
-      if (lane >= 8) lenp = 0;
-      const uint32_t incp = wave_scan_dpp(lenp);
-      const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
-      if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
-      for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
-    }
-    __syncthreads();
-    if (on) {
-      or_bits(lw, r + pre, ch[0], cl[0]);
-      or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
-    }
-    if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
-    __syncthreads();
-    const bool last = t + 1 == ntiles;
-    const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
-    for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
-    if (last) {
-      const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
-      for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
-    }
-    }
-  } else if (f == 3u && tid == 0) {  // timed out: sticky, whenever the tree's own status lands
-    __hip_atomic_store(reinterpret_cast<uint32_t *>(&meta[kAbort]), 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-    if (status) __hip_atomic_store(status, (int32_t)MH_ERR_HIP, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-  }
-finish:
-#if MH_CODE_STAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-  MH_CODE_STAMP(t + 1, 4)
-#endif
-  finish_launch(meta, tstate, claim, ntiles, kCodeThreads);
+  __syncthreads();  // tab
+  pack_emit(t, ncode, E, tab, q, qp, b, on, offsets + (uint64_t)f * nb,
+            reinterpret_cast<uint32_t *>(codes + f * codes_stride));
 }
 
-__global__ void __launch_bounds__(kCodeThreads, MH_CODE_MIN_WAVES) enc_one_kernel(
-    uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta, uint64_t *codes_len_out, uint64_t codes_cap,
-    int32_t *status, const Pixels px, uint64_t nb, uint32_t ntiles, uint64_t *tstate, uint32_t *claim,
-    uint32_t *offsets, uint32_t *words, uint8_t *block_init, uint64_t *thw) {
-  __shared__ uint32_t s_h[256 * kHistCopies];  // one tile's symbol counts, kHistCopies copies
-  if (blockIdx.x == 0) {
-    MH_CODE_STAMP(0, 0)
-    wait_histograms(px, nb, ntiles, hist, meta, claim, thw, s_h);
-    MH_CODE_STAMP(0, 1)
-    tree_body<true>(hist, canon_out, table, meta, codes_len_out, codes_cap, status, nb * 64);
-    MH_CODE_STAMP(0, 2)
-    // tree_body ends with the 256 symbol threads (the other waves have exited)
-    finish_launch(meta, tstate, claim, ntiles, 256);
-    return;
-  }
-  pack_tile_one(blockIdx.x - 1, px, hist, table, meta, tstate, claim, nb, ntiles, offsets, words, status, s_h,
-                block_init, thw);
+struct BatchWorkspace {  // per-frame slices, each part 256-B aligned
+  uint64_t *hist;       // n x kHistParts x 256
+  uint32_t *table;      // n x 256
+  uint64_t *meta;       // n x kMetaWords
+  uint16_t *tile_hist;  // n x ncode x 256
+  uint32_t *tile_off;   // n x (ncode + 1)
+};
+
+uint64_t carve_batch(uint8_t *base, uint64_t nb, uint32_t n, BatchWorkspace *w) {
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  uint64_t o = 0;
+  if (w) w->hist = reinterpret_cast<uint64_t *>(base + o);
+  o += align256((uint64_t)n * kHistParts * 256 * 8);
+  if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
+  o += align256((uint64_t)n * 256 * 4);
+  if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
+  o += align256((uint64_t)n * kMetaWords * 8);
+  if (w) w->tile_hist = reinterpret_cast<uint16_t *>(base + o);
+  o += align256((uint64_t)n * ncode * 256 * 2);
+  if (w) w->tile_off = reinterpret_cast<uint32_t *>(base + o);
+  o += align256((uint64_t)n * (ncode + 1) * 4);
+  return o;
 }
 
 }  // namespace
 
 extern "C" {
 
-// Frames of <= MH_FUSED_MAX_TILES code tiles take the two-launch path by default
+// Frames of <= kFusedMaxTiles code tiles take the two-launch path by default
 // (enc_split_kernel tiled, then enc_code_kernel: the tree in workgroup 0 while the
-// packers sum the earlier tiles' histograms). MH_ENCODE_KERNELS=1 selects the
-// one-launch path (enc_one_kernel: pixels read once, 0.6x the PMC traffic, but its
-// cross-XCD exchanges sit on the critical path: 3x slower, profiles/r03_encoder_one_launch_ab.txt),
-// =4 the four-kernel path (split, tree, scan, pack) for every size; larger frames
-// always take the four-kernel path.
+// packers sum the earlier tiles' histograms); larger frames take the four-kernel path
+// (split, tree, scan, pack). MH_ENCODE_KERNELS=4 forces the four-kernel path for
+// every size (A/B, tested); any other value keeps the default.
 static int encode_kernels() {
   static const int k = [] {
     const char *v = std::getenv("MH_ENCODE_KERNELS");
-    return v ? std::atoi(v) : 2;
+    return v && std::strcmp(v, "4") == 0 ? 4 : 2;
   }();
   return k;
 }
@@ -1627,39 +1234,30 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   if (g256 == 0 || ntiles > 0xFFFFFFFFull) return MH_ERR_CAPACITY;
 
   const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
-  // the tree zeroes the histogram after reading it and the one-launch path's last
-  // workgroup its state, for the next call
-  // meta .. claim .. tile_hist are contiguous (carve)
-  const size_t state_bytes =
-      align256((kGen + 1) * 8) + align256(ncode * 8) + align256(ncode * 4) + align256(ncode * 256 * 4);
-  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) &&
-      (hipMemsetAsync(w.hist, 0, kHistParts * 256 * 8, s) != hipSuccess ||
-       hipMemsetAsync(w.meta, 0, state_bytes, s) != hipSuccess))
+  // Per-call state: the tree zeroes the histogram after reading it, and the fused
+  // path's table words carry a call tag from meta[kGen], which the split kernel
+  // advances. Without MH_ENCODE_WORKSPACE_ZEROED the histogram, the code table and meta
+  // are zeroed (contiguous, one memset): a zeroed table word carries tag 0, which no
+  // call uses, so a packer can never take the previous call's table for this call's.
+  const size_t state_bytes = align256(kHistParts * 256 * 8) + align256(256 * 4) + align256((kGen + 1) * 8);
+  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) && hipMemsetAsync(w.hist, 0, state_bytes, s) != hipSuccess)
     return MH_ERR_HIP;
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0) ? 1u : 0u;
   const int path = encode_kernels();
-  if (ncode <= MH_FUSED_MAX_TILES && path == 1) {
-    const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
-    hipLaunchKernelGGL(enc_one_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist, d_canon_header,
-                       w.table, w.meta, d_codes_len, codes_cap, d_status, px, nb, (uint32_t)ncode, w.tstate, w.claim,
-                       d_block_offsets, reinterpret_cast<uint32_t *>(d_codes), d_block_init,
-                       reinterpret_cast<uint64_t *>(w.tile_hist));
-    return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
-  }
-  if (ncode <= MH_FUSED_MAX_TILES && path == 2) {
+  if (ncode <= kFusedMaxTiles && path == 2) {
     // two launches: the tiled split, then tree + offsets + packing in one kernel
     hipLaunchKernelGGL(enc_split_kernel, dim3((uint32_t)ncode), dim3(256), 0, s, d_gray, width, height, bw, nb,
-                       flags, vec, nullptr, d_block_init, w.hist, w.tile_hist, w.meta);
+                       flags, vec, nullptr, d_block_init, w.hist, w.tile_hist, w.meta, (uint32_t)ncode, 0ull);
     const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
     hipLaunchKernelGGL(enc_code_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist,
                        d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, px, w.tile_hist, nb,
                        (uint32_t)ncode, d_block_offsets, reinterpret_cast<uint32_t *>(d_codes));
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
-  const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, MH_SPLIT_WGS);
+  const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, kSplitWgs);
   hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
-                     w.sym, d_block_init, w.hist, nullptr, w.meta);
+                     w.sym, d_block_init, w.hist, nullptr, w.meta, 0u, 0ull);
   hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
                      d_codes_len, codes_cap, d_status, nb * 64);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
@@ -1694,6 +1292,49 @@ int mh_encode_frame_device(const uint8_t *d_gray, uint32_t width, uint32_t heigh
   std::memcpy(canon_header, host, 256);
   std::memcpy(codes_len, host + 256, 8);
   return MH_OK;
+}
+
+size_t mh_encode_frames_workspace_bytes(uint32_t width, uint32_t height, uint32_t n_frames) {
+  const uint64_t nb = (uint64_t)((width + 7) / 8) * ((height + 7) / 8);
+  return (size_t)carve_batch(nullptr, nb, n_frames, nullptr);
+}
+
+int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_stride, uint32_t n_frames,
+                                  uint32_t width, uint32_t height, uint32_t flags, uint8_t *d_canon_headers,
+                                  uint8_t *d_codes, uint64_t codes_frame_stride, uint64_t *d_codes_len,
+                                  uint64_t *d_frame_code_offsets, uint32_t *d_block_offsets, uint8_t *d_block_init,
+                                  int32_t *d_status, void *d_workspace, size_t workspace_bytes, void *stream) {
+  if (!d_gray || !d_canon_headers || !d_codes || !d_block_offsets || !d_workspace || !n_frames)
+    return MH_ERR_INVALID_ARG;
+  if (flags & ~(MH_FLAG_NO_DELTA | MH_ENCODE_WORKSPACE_ZEROED)) return MH_ERR_INVALID_ARG;
+  if (!width || !height || width > MH_MAX_DIM || height > MH_MAX_DIM) return MH_ERR_DIMS;
+  if (((uintptr_t)d_codes & 15u) || (codes_frame_stride & 15u) || ((uintptr_t)d_workspace & 255u))
+    return MH_ERR_ALIGN;
+  if (gray_frame_stride < (uint64_t)width * height && n_frames > 1) return MH_ERR_CAPACITY;
+  const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
+  const uint64_t nb = (uint64_t)bw * bh;
+  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  if (ncode * n_frames > 0x7FFFFFFFull || n_frames > 0x7FFFFFFFu) return MH_ERR_CAPACITY;
+  if (workspace_bytes < mh_encode_frames_workspace_bytes(width, height, n_frames)) return MH_ERR_CAPACITY;
+  BatchWorkspace w;
+  carve_batch(static_cast<uint8_t *>(d_workspace), nb, n_frames, &w);
+  hipStream_t s = (hipStream_t)stream;
+  // the trees re-zero the histograms they consumed; without the flag they are zeroed here
+  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) &&
+      hipMemsetAsync(w.hist, 0, (size_t)n_frames * kHistParts * 256 * 8, s) != hipSuccess)
+    return MH_ERR_HIP;
+  flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
+  const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
+  const uint32_t nt = (uint32_t)(ncode * n_frames);
+  hipLaunchKernelGGL(enc_split_kernel, dim3(nt), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
+                     nullptr, d_block_init, w.hist, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
+  hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(n_frames), dim3(kTreeThreads), 0, s, w.hist, d_canon_headers,
+                     w.table, w.meta, d_codes_len, codes_frame_stride, d_status, nb, w.tile_hist, (uint32_t)ncode,
+                     w.tile_off, d_frame_code_offsets, n_frames);
+  const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
+  hipLaunchKernelGGL(enc_pack_batch_kernel, dim3(nt), dim3(kCodeThreads), 0, s, px, gray_frame_stride, nb,
+                     (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes, codes_frame_stride);
+  return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
 }  // extern "C"

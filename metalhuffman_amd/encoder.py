@@ -145,6 +145,87 @@ class AsyncEncodedFrame:
                                   self.block_offsets, self.block_init, self.flags)
 
 
+class BatchEncoder:
+    """n_frames frames of one size per call (mh_encode_frames_device_async): each frame
+    gets its own histogram, tree and codes (byte-identical to codec.encode_frame, frame
+    by frame), in three launches whatever n_frames. Codes land in fixed 16-byte
+    aligned slots of `slot` bytes (the capacity), so the result is one DeviceFrames
+    batch for decode() when the frames share a table (e.g. block shuffles)."""
+
+    def __init__(self, width: int, height: int, n_frames: int, device="cuda"):
+        self.device = _dev(device)
+        self.width, self.height, self.n = width, height, n_frames
+        bw, bh = block_grid(width, height)
+        self.nb = bw * bh
+        ws = int(N.lib().mh_encode_frames_workspace_bytes(width, height, n_frames))
+        # zero-filled once: every call leaves the histograms zeroed (MH_ENCODE_WORKSPACE_ZEROED)
+        self.workspace = torch.zeros(ws + 256, dtype=torch.uint8, device=self.device)
+        self.slot = (self.nb * 64 * 2 + N.MH_CODES_PAD + 15) // 16 * 16 + 16
+
+    def encode_async(self, grays: torch.Tensor, flags: int = 0, init_zero_delta: bool = False,
+                     stream: Optional[torch.cuda.Stream] = None) -> "AsyncEncodedBatch":
+        """grays: contiguous uint8 [n, H, W] on the encoder's device, ready on `stream`."""
+        if (grays.dtype != torch.uint8 or tuple(grays.shape) != (self.n, self.height, self.width)
+                or not grays.is_contiguous()):
+            raise ValueError(f"grays must be contiguous uint8 [{self.n}, {self.height}, {self.width}]")
+        if grays.device != self.device:
+            raise ValueError("grays must live on the encoder's device")
+        n = self.n
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            codes = torch.empty(n * self.slot + 16, dtype=torch.uint8, device=self.device)
+            offs = torch.empty(n * self.nb, dtype=torch.int32, device=self.device)
+            init = torch.empty(n * self.nb, dtype=torch.uint8, device=self.device) if init_zero_delta else None
+            canon = torch.empty((n, 256), dtype=torch.uint8, device=self.device)
+            lens = torch.empty(n, dtype=torch.int64, device=self.device)
+            fco = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+            status = torch.empty(n, dtype=torch.int32, device=self.device)
+        cbase = (codes.data_ptr() + 15) // 16 * 16
+        base = self.workspace.data_ptr()
+        aligned = (base + 255) // 256 * 256
+        N.check(N.lib().mh_encode_frames_device_async(
+            grays.data_ptr(), self.height * self.width, n, self.width, self.height,
+            flags | N.MH_ENCODE_WORKSPACE_ZEROED, canon.data_ptr(), cbase, self.slot, lens.data_ptr(),
+            fco.data_ptr(), offs.data_ptr(), init.data_ptr() if init is not None else None, status.data_ptr(),
+            aligned, self.workspace.numel() - (aligned - base), _stream_ptr(stream, self.device)),
+            "mh_encode_frames_device_async")
+        view = codes[cbase - codes.data_ptr(): cbase - codes.data_ptr() + n * self.slot]
+        return AsyncEncodedBatch(self.width, self.height, n, self.slot, canon, view, lens, fco, status, offs,
+                                 init, flags)
+
+
+@dataclasses.dataclass
+class AsyncEncodedBatch:
+    """A batched encode in flight: everything on the device (per-frame slots)."""
+    width: int
+    height: int
+    n_frames: int
+    slot: int
+    canon: torch.Tensor               # u8[n, 256]
+    codes: torch.Tensor               # u8[n * slot]
+    codes_len: torch.Tensor           # int64[n] (payload + MH_CODES_PAD; 0 on an error)
+    frame_code_offsets: torch.Tensor  # int64[n + 1] = f * slot
+    status: torch.Tensor              # int32[n]
+    block_offsets: torch.Tensor       # int32 view of u32[n * NB]
+    block_init: Optional[torch.Tensor]
+    flags: int
+
+    def frames(self) -> DeviceFrames:
+        """All slots as one DeviceFrames batch (valid when the frames share a table)."""
+        return DeviceFrames(self.width, self.height, self.n_frames, self.block_offsets, self.codes,
+                            self.frame_code_offsets, self.block_init, self.flags,
+                            int(self.codes.numel()) - self.n_frames * N.MH_CODES_PAD)
+
+    def frame(self, f: int) -> DeviceEncodedFrame:
+        """Frame f (synchronises; raises MHError on a rejected frame)."""
+        st, n = int(self.status[f].item()), int(self.codes_len[f].item())
+        N.check(st, "mh_encode_frames_device_async")
+        nb = self.block_offsets.numel() // self.n_frames
+        init = self.block_init[f * nb:(f + 1) * nb] if self.block_init is not None else None
+        return DeviceEncodedFrame(self.width, self.height, self.canon[f].cpu().numpy(),
+                                  self.codes[f * self.slot: f * self.slot + n],
+                                  self.block_offsets[f * nb:(f + 1) * nb], init, self.flags)
+
+
 def encode_frame_device(gray: torch.Tensor, flags: int = 0, init_zero_delta: bool = False) -> DeviceEncodedFrame:
     """One-shot GPU encode of a [H, W] uint8 device tensor."""
     h, w = gray.shape

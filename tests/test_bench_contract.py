@@ -29,7 +29,7 @@ def test_metric_is_baselines(bench):
 
 def test_default_arguments(bench):
     a = bench.parse_args([])
-    assert (a.gpus, a.workload, a.frames, a.batch) == (1, "frame", 64, 64)
+    assert (a.gpus, a.workload, a.frames, a.batch) == (1, "frame", 128, 64)  # two cold batch launches
     assert a.steps > 0 and a.warmup >= 0 and not a.no_graph
     a = bench.parse_args(["--gpus", "8", "--steps", "20", "--warmup", "5"])
     assert (a.gpus, a.steps, a.warmup) == (8, 20, 5)

@@ -291,7 +291,7 @@ def test_async_encode_workspace_flag(mh, device, bigbridge):
         assert np.array_equal(r.canon, ref.canon) and np.array_equal(r.codes.cpu().numpy(), ref.codes), k
 
 
-@pytest.mark.parametrize("path", ["2", "1"])
+@pytest.mark.parametrize("path", ["2"])
 def test_fused_encoder_timeout_is_sticky(mh, path):
     """A packing workgroup that gives up waiting for the code table (diagnostic build
     with a zero spin budget, MH_DIAG_SPIN_TICKS=0) must leave MH_ERR_HIP in the status,
@@ -327,12 +327,12 @@ def test_fused_encoder_timeout_is_sticky(mh, path):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("path", ["1", "4"])
+@pytest.mark.parametrize("path", ["4", "1"])
 def test_encoder_alternative_paths(mh, path):
-    """The two-launch path is the default for frames of <= 512 code tiles; the one-launch
-    (MH_ENCODE_KERNELS=1: enc_one_kernel) and four-kernel (=4) paths stay selectable and
-    byte-identical to the host codec. The knob is read once per process, so each path
-    runs in a child process."""
+    """The two-launch path is the default for frames of <= 512 code tiles; the
+    four-kernel path (MH_ENCODE_KERNELS=4) stays selectable and byte-identical to the
+    host codec; any other value (the removed one-launch path's "1" included) keeps the
+    default. The knob is read once per process, so each path runs in a child process."""
     import os
     import subprocess
     import sys
@@ -360,36 +360,44 @@ def test_encoder_alternative_paths(mh, path):
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
-def test_one_launch_claim_fallback(mh):
-    """The one-launch encoder's deadlock guard: workgroup 0 counts the tiles whose own
-    workgroups have not published their counts when its wait ends. A diagnostic build
-    with no wait at all (MH_ONE_CLAIM_TICKS=0) takes that path on most tiles of every
-    frame; the bytes must not change (child process, MH_LIB)."""
+@pytest.mark.parametrize("path", ["2", "4"])
+def test_async_encode_unzeroed_workspace_twice(mh, path):
+    """without MH_ENCODE_WORKSPACE_ZEROED every call zeroes its per-call
+    state. Two flags=0 calls on one workspace with DIFFERENT images must each give the
+    host codec's bytes: the second call's packers must not take the first call's code
+    table (whose words carried the same call tag before the table was zeroed too).
+    Child process per path (MH_ENCODE_KERNELS is read once)."""
     import os
     import subprocess
     import sys
 
     import metalhuffman_amd.build as B
-    lib = B.diag_lib_path("claim0")
-    assert os.path.exists(lib), "build() makes the diagnostic libraries"
     code = (
-        "import sys, numpy as np, torch; sys.path.insert(0, %r)\n"
+        "import sys, ctypes, numpy as np, torch; sys.path.insert(0, %r)\n"
         "import metalhuffman_amd as mh\n"
-        "from metalhuffman_amd import frames as F\n"
+        "from metalhuffman_amd import _native as N, frames as F\n"
         "from metalhuffman_amd.encoder import Encoder\n"
-        "assert mh.lib().mh_build_stamp().decode().startswith('diag:claim0:')\n"
         "bb = F.bigbridge()\n"
-        "for img, init in ((bb, False), (np.ascontiguousarray(bb[:777, :1001]), True)):\n"
-        "    ref = mh.encode_frame(img, init_zero_delta=init)\n"
-        "    enc = Encoder(img.shape[1], img.shape[0], 'cuda:0')\n"
-        "    for _ in range(3):\n"
-        "        a = enc.encode_async(torch.from_numpy(np.ascontiguousarray(img)).to('cuda:0'), 0, init)\n"
-        "        r = a.result()\n"
-        "        assert np.array_equal(r.canon, ref.canon)\n"
-        "        assert np.array_equal(r.codes.cpu().numpy(), ref.codes)\n"
-        "        assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), ref.block_offsets)\n"
-        "        if init: assert np.array_equal(a.block_init.cpu().numpy(), ref.block_init)\n"
+        "imgs = [bb, F.uniform_random(2048, 1536, 9), np.ascontiguousarray(F.block_shuffle(bb, 3)), bb]\n"
+        "enc = Encoder(2048, 1536, 'cuda:0')\n"
+        "codes = torch.empty(enc.cap, dtype=torch.uint8, device='cuda:0')\n"
+        "offs = torch.empty(enc.nb, dtype=torch.int32, device='cuda:0')\n"
+        "canon = torch.empty(256, dtype=torch.uint8, device='cuda:0')\n"
+        "meta = torch.zeros(2, dtype=torch.int64, device='cuda:0')\n"
+        "base = enc.workspace.data_ptr(); al = (base + 255) // 256 * 256\n"
+        "for img in imgs:\n"
+        "    ref = mh.encode_frame(img)\n"
+        "    d = torch.from_numpy(np.ascontiguousarray(img)).to('cuda:0')\n"
+        "    N.check(N.lib().mh_encode_frame_device_async(d.data_ptr(), 2048, 1536, 0, canon.data_ptr(),\n"
+        "        codes.data_ptr(), codes.numel(), meta.data_ptr(), offs.data_ptr(), None, meta.data_ptr() + 8, al,\n"
+        "        enc.workspace.numel() - (al - base), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), 'enc')\n"
+        "    torch.cuda.synchronize()\n"
+        "    n = int(meta[0].item())\n"
+        "    assert int(meta[1].item()) == 0, int(meta[1].item())\n"
+        "    assert np.array_equal(canon.cpu().numpy(), ref.canon)\n"
+        "    assert n == ref.codes.size and np.array_equal(codes[:n].cpu().numpy(), ref.codes)\n"
+        "    assert np.array_equal(offs.cpu().numpy().view(np.uint32), ref.block_offsets)\n"
         "print('ok')\n" % B.ROOT)
-    env = dict(os.environ, MH_LIB=lib, MH_ENCODE_KERNELS="1")
+    env = dict(os.environ, MH_ENCODE_KERNELS=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -78,3 +78,38 @@ def test_host_device_chain(host_bin, wh):
     r = _run([host_bin, "device", str(wh[0]), str(wh[1]), "5"])
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith(f"device ok {wh[0]} {wh[1]} "), r.stdout
+
+
+@pytest.fixture(scope="module")
+def multi_bin(mh):
+    import metalhuffman_amd.build as B
+    return B.build_host_multi()
+
+
+def test_multi_host_builds_and_prints_usage(multi_bin):
+    """The multi-GPU C host links against RCCL and the C-ABI (no GPU needed)."""
+    r = _run([multi_bin])
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+@pytest.mark.gpu
+def test_multi_host_rccl_world1(multi_bin, bigbridge, tmp_path):
+    """host/mh_decode_multi at N = 1 on the box: RCCL
+    communicator over the device, ncclBroadcast of device 0's 256-byte header, device
+    table build, a 64-frame shard of BigBridge block shuffles encoded on the device in
+    one batched call (every header equal to the broadcast one), batch decodes timed,
+    every raster equal to its input. The same binary runs N = 2..8 on a full node."""
+    p = tmp_path / "bb.gray"
+    p.write_bytes(np.ascontiguousarray(bigbridge).tobytes())
+    h, w = bigbridge.shape
+    r = _run([multi_bin, "1", "64", "8", str(w), str(h), str(p)], timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("multi ok 1 devices 64 frames_per_device 2048 1536"), r.stdout
+    mbps = float(r.stdout.split("MBps_events ")[1].split()[0])
+    assert mbps > 1e5, r.stdout  # a 64-frame launch decodes >> 1e5 MB/s on one MI355X
+
+
+@pytest.mark.gpu
+def test_multi_host_synthetic_small(multi_bin):
+    r = _run([multi_bin, "1", "3", "2"], timeout=240)
+    assert r.returncode == 0 and r.stdout.startswith("multi ok 1 devices 3 "), r.stdout + r.stderr
