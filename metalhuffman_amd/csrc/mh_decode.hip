@@ -66,6 +66,9 @@ struct DecodeArgs {
   uint32_t w, h, bw, bh, nb;
   uint32_t tiles_per_frame, total_tiles;
   uint32_t n_groups;           // ceil(total_tiles / waves_per_wg)
+  uint32_t nwaves, grid;       // batch kernel launch shape as kernel arguments: blockDim / gridDim
+                               // read the dispatch packet's implicit arguments, a dependent
+                               // global load at the head of the kernel (code object v5)
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
@@ -566,13 +569,13 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
 // Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
 // header of tile i+2 and the code span of tile i+1 are in flight into registers;
 // the span is written to the wave's LDS window once tile i has finished reading it.
-template <bool kDelta, class Cfg>
+template <bool kDelta>
 __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
-  constexpr bool kSwz = Cfg::kSwz;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwaves = blockDim.x >> 6;
-  const uint32_t gstride = gridDim.x * nwaves;
+  const uint32_t nwaves = a.nwaves;
+  const uint32_t nthreads = nwaves * 64u;
+  const uint32_t gstride = a.grid * nwaves;
   uint8_t *stage = s_stage + wave * kStageBytes;
   const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
 #if MH_DIAG_STAMPS
@@ -586,12 +589,24 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
   hdr_issue(a, t0, lane, hc);
+  // The step flavour, from the prepared table's code lengths (kernel-uniform): issued
+  // behind the first header, and only waited for at the first tile's decode, so no
+  // dependent load sits in front of the header (one flavour switch per tile).
+  //   2: one code length (flat) -> escape-free step, swizzled stage
+  //   1: no code over 13 bits   -> escape-free step
+  //   0: general step (escapes), also for an in-kernel table
+  uint32_t mx = 16, mn = 0;
+  if (a.lut) {
+    const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
+    mx = ml[0];
+    mn = ml[1];
+  }
 
   // ---- lookup table into LDS (shared by the workgroup) ----
   if (a.lut) {
     const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += blockDim.x) dstv[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += nthreads) dstv[i] = src[i];
   }
 
   v4u32 R[kStageChunks];
@@ -604,10 +619,14 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   if (a.lut) {
     __syncthreads();
   } else {
-    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, blockDim.x, [] { __syncthreads(); });
+    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, nthreads, [] { __syncthreads(); });
   }
   MH_STAMP(2);
-  if (cur_staged) span_write<kSwz>(cur, lane, R, stage);
+  const uint32_t flavor = !a.lut ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
+  if (cur_staged) {
+    if (flavor == 2) span_write<true>(cur, lane, R, stage);
+    else span_write<false>(cur, lane, R, stage);
+  }
   MH_STAMP(3);
   // Resolved even past the end (zero-record loads): every Tile field is defined
   // before span_issue builds a descriptor from it.
@@ -631,14 +650,22 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
       LdsWords src{stage};
       // waves with more tiles left run first (the arbiter otherwise favours the oldest)
       set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
-      decode_block<kDelta, Cfg>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
+      if (flavor == 1)
+        decode_block<kDelta, Lut13NoEsc>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
+      else if (flavor == 2)
+        decode_block<kDelta, Lut13Flat>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
+      else
+        decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
     }
 #if MH_DIAG_STAMPS
     if (first_tile) MH_STAMP(4);
     first_tile = false;
 #endif
     wave_sync();  // this tile's reads -> next tile's staging writes
-    if (nxt_staged) span_write<kSwz>(nxt, lane, R, stage);
+    if (nxt_staged) {
+      if (flavor == 2) span_write<true>(nxt, lane, R, stage);
+      else span_write<false>(nxt, lane, R, stage);
+    }
     const Tile nn = hdr_resolve(a, hn, lane);
     cur = nxt;
     cur_staged = nxt_staged;
@@ -654,7 +681,8 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
     hdr_issue(a, t, lane, h);
     const Tile tt = hdr_resolve(a, h, lane);
     const OutTile ot = out_tile(a, tt, lane);
-    decode_halves<kDelta, Cfg>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+    if (flavor == 2) decode_halves<kDelta, Lut13Flat>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+    else decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
   }
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
@@ -674,18 +702,7 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
 // swizzled stage. An in-kernel table (no prepared LUT) keeps the general step.
 template <bool kDelta>
 __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(const DecodeArgs a) {
-  uint32_t mx = 16, mn = 0;
-  if (a.lut) {
-    const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
-    mx = ml[0];
-    mn = ml[1];
-  }
-  if (a.lut && mx == mn)
-    batch_tiles<kDelta, Lut13Flat>(a);
-  else if (a.lut && mx <= (uint32_t)kLutBits)
-    batch_tiles<kDelta, Lut13NoEsc>(a);
-  else
-    batch_tiles<kDelta, Lut13>(a);
+  batch_tiles<kDelta>(a);
 }
 
 // ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------
@@ -704,7 +721,7 @@ template <bool kDelta>
 __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwaves = blockDim.x >> 6;
+  constexpr uint32_t nwaves = kSmallWaves;  // launched with kSmallWaves waves per workgroup
   uint8_t *stage = s_stage + wave * kStageBytes;
   const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut_small);
   const uint8_t *prepared = reinterpret_cast<const uint8_t *>(a.lut);
@@ -1185,6 +1202,8 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   a.n_groups = (a.total_tiles + nw - 1) / nw;
   const uint32_t resident = (uint32_t)(cus * di->occ[kDelta ? 1 : 0][nw]);
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
+  a.nwaves = nw;
+  a.grid = grid;
   MH_LAUNCH(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), s, any_order, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }

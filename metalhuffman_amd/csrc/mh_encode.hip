@@ -1236,10 +1236,13 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
   // Per-call state: the tree zeroes the histogram after reading it, and the fused
   // path's table words carry a call tag from meta[kGen], which the split kernel
-  // advances. Without MH_ENCODE_WORKSPACE_ZEROED the histogram, the code table and meta
-  // are zeroed (contiguous, one memset): a zeroed table word carries tag 0, which no
-  // call uses, so a packer can never take the previous call's table for this call's.
-  const size_t state_bytes = align256(kHistParts * 256 * 8) + align256(256 * 4) + align256((kGen + 1) * 8);
+  // advances once per call. Without MH_ENCODE_WORKSPACE_ZEROED the histogram, the code
+  // table and meta[0 .. kGen) are zeroed (contiguous, one memset), meta[kGen] is NOT:
+  // a zeroed (or garbage-free) table word carries tag 0, which no call uses, and the
+  // tag still differs from the previous call's, so a packer can take neither the
+  // previous call's table words -- even from a stale cache line -- nor a cleared one.
+  // (zeroing meta[kGen] too gave every call the same tag.)
+  const size_t state_bytes = align256(kHistParts * 256 * 8) + align256(256 * 4) + kGen * 8;
   if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) && hipMemsetAsync(w.hist, 0, state_bytes, s) != hipSuccess)
     return MH_ERR_HIP;
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
