@@ -238,8 +238,8 @@ size_t mh_encode_frames_workspace_bytes(uint32_t width, uint32_t height, uint32_
  * mh_frame batch for mh_decode (all frames must share one canonical table to be
  * decoded in one launch, e.g. block shuffles of one image). A rejected frame writes
  * no codes or offsets and does not affect the others. d_workspace: 256-byte aligned,
- * mh_encode_frames_workspace_bytes(); MH_ENCODE_WORKSPACE_ZEROED as for
- * mh_encode_frame_device_async (every call leaves the histograms zeroed).
+ * mh_encode_frames_workspace_bytes(), any content (every part is written before it
+ * is read within the call; MH_ENCODE_WORKSPACE_ZEROED is accepted and changes nothing).
  * Asynchronous on `stream`; the return value covers argument checks and launches. */
 int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_stride, uint32_t n_frames,
                                   uint32_t width, uint32_t height, uint32_t flags, uint8_t *d_canon_headers,

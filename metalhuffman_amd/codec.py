@@ -11,8 +11,10 @@ Differences from the reference, by design:
     canonical header explicitly;
   * errors raise MHError instead of assert() (e.g. a code deeper than 16 bits,
     HuffmanEncoder.cpp:131);
-  * the CPU decoders (decodeHuffmanBits*) are not part of the product: the GPU
-    decoder is the decode path; the CPU restatement lives in oracle/ as the checker.
+  * the CPU decoders (decodeHuffmanBits*, decode_frame_cpu) are product code in the
+    native library (csrc/mh_cpu.cpp, a threaded frame decoder for the reference's CPU
+    path); the GPU decoder is the hot path. Neither calls the CPU restatement in
+    oracle/, which stays the test-only checker.
 """
 from __future__ import annotations
 

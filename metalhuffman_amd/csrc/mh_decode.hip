@@ -513,6 +513,15 @@ __device__ __forceinline__ void span_write(const Tile &t, uint32_t lane, const v
   }
 }
 
+// A workgroup barrier for LDS-only hand-offs: waits for this wave's LDS operations
+// (lgkmcnt), not its global ones -- __syncthreads()'s workgroup-scope fence also waits
+// for every outstanding global load (vmcnt(0)), here the first header.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -588,6 +597,25 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
+  // ---- lookup table into LDS (shared by the workgroup) ----
+  // A fixed count of unconditional 16-B loads per thread (chunks past the table fall
+  // outside the descriptor and return 0), issued FIRST, all in flight together; the
+  // first header follows. The table is stored and the workgroup barrier passed as soon
+  // as the table's (L2) loads land -- an LDS-only barrier, so no wave waits there for
+  // another wave's (HBM, cold) header. Round 3's loop of dependent copies, behind the
+  // header, cost 3 L2 round trips plus the slowest header of the workgroup before the
+  // first span could be staged (profiles/r04_v3_tile_start_ab.txt). A launch with a
+  // prepared table has >= 5 waves per workgroup (smaller ones take the small-launch
+  // kernel), so 4 loads per thread cover the table.
+  constexpr uint32_t kLutChunks = kLutBytes / 16, kLutPer = 4;
+  const bool fixed_copy = a.lut && nthreads * kLutPer >= kLutChunks;
+  v4u32 L[kLutPer];
+  {
+    const __amdgpu_buffer_rsrc_t rl = uniform_rsrc(a.lut, fixed_copy ? (uint32_t)kLutBytes : 0u);
+#pragma unroll
+    for (uint32_t k = 0; k < kLutPer; ++k)
+      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * nthreads) * 16u), 0, 0);
+  }
   hdr_issue(a, t0, lane, hc);
   // The step flavour, from the prepared table's code lengths (kernel-uniform): issued
   // behind the first header, and only waited for at the first tile's decode, so no
@@ -601,12 +629,16 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
     mx = ml[0];
     mn = ml[1];
   }
-
-  // ---- lookup table into LDS (shared by the workgroup) ----
-  if (a.lut) {
+  if (fixed_copy) {
+    v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
+#pragma unroll
+    for (uint32_t k = 0; k < kLutPer; ++k)
+      if (threadIdx.x + k * nthreads < kLutChunks) dstv[threadIdx.x + k * nthreads] = L[k];
+    lds_barrier();
+  } else if (a.lut) {
     const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(kLutBytes / 16); i += nthreads) dstv[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < kLutChunks; i += nthreads) dstv[i] = src[i];
   }
 
   v4u32 R[kStageChunks];
@@ -616,7 +648,9 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   span_issue(a, cur, lane, R, cur_staged);
   hdr_issue(a, next_tile(t0), lane, hn);
 
-  if (a.lut) {
+  if (fixed_copy) {
+    // (table in LDS, barrier passed above)
+  } else if (a.lut) {
     __syncthreads();
   } else {
     build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, nthreads, [] { __syncthreads(); });

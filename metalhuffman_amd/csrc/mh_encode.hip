@@ -72,6 +72,17 @@ struct Workspace {  // carved out of the caller's workspace, 256-B aligned parts
 
 constexpr uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
+// A workgroup barrier for LDS-only hand-offs: waits for this wave's LDS operations
+// (lgkmcnt), not its global ones. __syncthreads()'s workgroup-scope fence also waits
+// for every outstanding global load and store (vmcnt(0)) -- in the packers that put an
+// HBM write round trip (the offsets, the code words) and any prefetch behind every
+// barrier. Valid wherever the threads of a workgroup exchange data only through LDS.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
   uint64_t o = 0;
   const uint64_t ntiles = (nb + kScanTile - 1) / kScanTile;
@@ -111,7 +122,9 @@ constexpr uint32_t kSplitWgs = 256;   // split workgroups (four-kernel path): on
 __device__ __forceinline__ uint64_t block_row(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw,
                                               uint64_t nb, uint32_t vec, uint64_t b, uint32_t r) {
   if (b >= nb) return 0;
-  const uint32_t bx = (uint32_t)(b % bw), y = (uint32_t)(b / bw) * 8 + r;
+  // a frame has < 2^26 blocks (65535^2 / 64): 32-bit division (a 64-bit one is a long
+  // software sequence per lane)
+  const uint32_t b32 = (uint32_t)b, bx = b32 % bw, y = (b32 / bw) * 8 + r;
   if (y >= H) return 0;
   const uint8_t *row = gray + (uint64_t)y * W + bx * 8u;
   if (vec) return *reinterpret_cast<const uint64_t *>(row);  // W % 8 == 0, 8-byte aligned frame
@@ -163,7 +176,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     wg = blockIdx.x - f * ncode;
     gray += f * gray_stride;
     if (block_init) block_init += (uint64_t)f * nb;
-    hist += (uint64_t)f * kHistParts * 256;
+    if (hist) hist += (uint64_t)f * kHistParts * 256;
     tile_hist += (uint64_t)f * ncode * 256;
   }
   if (tiled && meta && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
@@ -174,7 +187,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   MH_SPLIT_STAMP(0)
   __shared__ uint32_t h[256 * kHistCopies];
   for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t r = threadIdx.x & 7u;
   const uint32_t copy = threadIdx.x % kHistCopies;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
@@ -218,14 +231,15 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     }
   }
   MH_SPLIT_STAMP(2)
-  __syncthreads();
+  lds_barrier();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
   if (tiled) tile_hist[(uint64_t)wg * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
   MH_SPLIT_STAMP(3)
   // kHistParts partial histograms (workgroups round-robin over them, as over the
   // XCDs): one address per bin would serialise every workgroup's atomic on it
-  if (c) atomicAdd((unsigned long long *)&hist[(wg % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
+  // (the batched path passes no hist: its tree kernel sums the tile counts itself)
+  if (c && hist) atomicAdd((unsigned long long *)&hist[(wg % kHistParts) * 256 + threadIdx.x], (unsigned long long)c);
 #if MH_CODE_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   MH_SPLIT_STAMP(4)
@@ -372,9 +386,12 @@ template <bool kFused>
 // Returns, to the 256 symbol threads, symbol tid's table entry (code_lj16 << 16 | len;
 // 0 for an absent symbol) with bit 7 set when the frame is rejected; the other
 // threads return 0 early (before the symbol threads' last barriers).
+// counts (optional): the 256 symbol counts already in LDS (the batched path sums its
+// tile counts itself); otherwise they are the sum of hist's kHistParts partial
+// histograms, which are left zeroed.
 __device__ __forceinline__ uint32_t tree_body(uint64_t *hist, uint8_t *canon_out, uint32_t *table, uint64_t *meta,
                                           uint64_t *codes_len_out, uint64_t codes_cap, int32_t *status,
-                                          uint64_t nsym) {
+                                          uint64_t nsym, const uint32_t *counts = nullptr) {
   constexpr uint32_t kEnd = 0xFFFFFFFFu;  // empty queue slot
   constexpr uint32_t kW32End = (1u << 22) - 1u;  // 32-bit merge keys: an empty slot's weight
   const bool k32 = nsym < (uint64_t)kW32End;
@@ -391,12 +408,16 @@ __device__ __forceinline__ uint32_t tree_body(uint64_t *hist, uint8_t *canon_out
   // round trip overlaps the histogram loads instead of preceding the publication
   const uint32_t tag = kFused && sym_thread ? table_tag(meta) : 0u;
   uint64_t f = 0;
-  if (sym_thread) {
+  if (sym_thread && counts) {
+    f = counts[tid];
+  } else if (sym_thread) {
 #pragma unroll
     for (uint32_t k = 0; k < kHistParts; ++k) f += hist[k * 256 + tid];
     // leave the histogram zeroed for the next frame's split (MH_ENCODE_WORKSPACE_ZEROED)
 #pragma unroll
     for (uint32_t k = 0; k < kHistParts; ++k) hist[k * 256 + tid] = 0;
+  }
+  if (sym_thread) {
     s_len[tid] = 0;
     s_lw[tid] = kEnd;
     s_iw[tid] = kEnd;
@@ -879,9 +900,24 @@ struct Pixels {  // the frame as the split reads it
 // computes those bits itself from that block's symbols and writes the word whole; a
 // tile leaves its own partial last word to the next tile (the last tile writes it and
 // the zero pad). Every code word is written exactly once: no clearing, no atomics.
+// Buffer descriptor from wave-uniform inputs (readfirstlane, so buffer ops need no
+// waterfall loop); offsets past `bytes` are dropped by the hardware.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t enc_rsrc(const void *base, uint64_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t n = (uint32_t)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
+constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past every descriptor's range: dropped
+
+// The stores are a fixed count of unconditional buffer stores per thread (lanes with
+// nothing to store use an out-of-range offset), so the compiler counts them exactly in
+// vmcnt and a persistent caller's prefetch for the next tile is never drained by them.
 __device__ __forceinline__ void pack_emit(uint32_t t, uint32_t ntiles, uint32_t E, const uint32_t *tab,
                                           uint64_t q, uint64_t qp, uint64_t b, bool on, uint32_t *offsets,
-                                          uint32_t *words) {
+                                          uint64_t nb, uint32_t *words, uint64_t words_bytes) {
   __shared__ uint32_t lw[kCodeWords];
   __shared__ uint32_t s_scan[kCodeWaves];
   const uint32_t tid = threadIdx.x, part = tid & 7u, lane = tid & 63u, wave = tid >> 6;
@@ -900,16 +936,17 @@ __device__ __forceinline__ void pack_emit(uint32_t t, uint32_t ntiles, uint32_t 
   // exclusive scan over the 1024 lanes (lane order = block order, eight lanes each)
   const uint32_t incl = wave_scan_dpp(nbits);
   if (lane == 63) s_scan[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   if (wave == 0) {
     const uint32_t v = wave_scan_dpp(lane < kCodeWaves ? s_scan[lane] : 0u);
     if (lane < kCodeWaves) s_scan[lane] = v;
   }
-  __syncthreads();
+  lds_barrier();
   const uint32_t pre = (wave ? s_scan[wave - 1] : 0u) + incl - nbits;
   const uint32_t T = s_scan[kCodeWaves - 1];
   MH_CODE_STAMP(t + 1, 4)
-  if (on && part == 0) offsets[b] = E + pre;
+  __builtin_amdgcn_raw_buffer_store_b32(E + pre, enc_rsrc(offsets, nb * 4u), (int)(on && part == 0 ? (uint32_t)b * 4u : kOob),
+                                        0, 0);
   const uint32_t r = E & 31u, w0 = E >> 5, end = E + T;
   const uint32_t nwords = ((end + 31u) >> 5) - w0;
   for (uint32_t i = tid; i < nwords; i += kCodeThreads) lw[i] = 0;
@@ -936,28 +973,34 @@ __device__ __forceinline__ void pack_emit(uint32_t t, uint32_t ntiles, uint32_t 
     if (lane < 8 && after < r) head = (uint32_t)(acc << (32u - r + after));
     for (uint32_t o = 1; o < 8; o <<= 1) head |= __shfl_xor(head, o);
   }
-  __syncthreads();
+  lds_barrier();
   if (on) {
     or_bits(lw, r + pre, ch[0], cl[0]);
     or_bits(lw, r + pre + cl[0], ch[1], cl[1]);
   }
   if (r && tid == 0) atomicOr(&lw[0], bswap32(head));
-  __syncthreads();
+  lds_barrier();
   MH_CODE_STAMP(t + 1, 5)
   // a partial last word belongs to the next tile (it adds its own first bits); the
   // last tile writes it, then the zero pad up to the byte count rounded to words
   const bool last = t + 1 == ntiles;
   const uint32_t nout = (!last && (end & 31u)) ? nwords - 1 : nwords;
-  for (uint32_t i = tid; i < nout; i += kCodeThreads) words[w0 + i] = lw[i];
-  if (last) {
-    const uint64_t nw = ((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u;
-    for (uint64_t i = (uint64_t)w0 + nwords + tid; i < nw; i += kCodeThreads) words[i] = 0;
+  const __amdgpu_buffer_rsrc_t rw = enc_rsrc(words, words_bytes);
+  constexpr uint32_t kOut = (kCodeWords + kCodeThreads - 1) / kCodeThreads;
+#pragma unroll
+  for (uint32_t k = 0; k < kOut; ++k) {
+    const uint32_t i = tid + k * kCodeThreads;
+    __builtin_amdgcn_raw_buffer_store_b32(lw[min(i, kCodeWords - 1u)], rw, (int)(i < nout ? (w0 + i) * 4u : kOob), 0, 0);
   }
+  // the last tile: the zero pad up to the byte count rounded to words (<= 3 words)
+  const uint32_t nw = (uint32_t)(((uint64_t)(end + 7u) / 8u + MH_CODES_PAD + 3u) / 4u);
+  const uint32_t ip = w0 + nwords + tid;
+  __builtin_amdgcn_raw_buffer_store_b32(0u, rw, (int)(last && ip < nw ? ip * 4u : kOob), 0, 0);
 }
 
 __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uint16_t *tile_hist,
                                           const uint32_t *table, uint64_t *meta, uint64_t nb, uint32_t ntiles,
-                                          uint32_t *offsets, uint32_t *words, int32_t *status) {
+                                          uint32_t *offsets, uint32_t *words, uint64_t codes_cap, int32_t *status) {
   __shared__ uint32_t tab[256];
   __shared__ uint32_t s_cnt[kCodeWaves][256];  // symbol counts of the tiles before this one, per wave
   __shared__ uint32_t s_dot[4];
@@ -1024,9 +1067,9 @@ __device__ __forceinline__ void pack_tile(uint32_t t, const Pixels px, const uin
     const uint32_t x = wave_scan_dpp(c * (tab[tid] & 0xFFu));
     if (lane == 63) s_dot[wave] = x;
   }
-  __syncthreads();
+  lds_barrier();
   const uint32_t E = s_dot[0] + s_dot[1] + s_dot[2] + s_dot[3];
-  pack_emit(t, ntiles, E, tab, q, qp, b, on, offsets, words);
+  pack_emit(t, ntiles, E, tab, q, qp, b, on, offsets, nb, words, codes_cap);
 #if MH_CODE_STAMPS
   if (tid == 0 && t + 1 < kCodeStampWgs)
     g_code_stamps[(t + 1) * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
@@ -1050,7 +1093,7 @@ __global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_code_kernel(u
     MH_CODE_STAMP(0, 3)
     return;
   }
-  pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, status);
+  pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, codes_cap, status);
 }
 
 // ---- batched frames: enc_split_kernel (tiled) + enc_tree_batch_kernel + enc_pack_batch_kernel
@@ -1075,14 +1118,46 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
     frame_off[f] = (uint64_t)f * codes_cap;
     if (f + 1 == n_frames) frame_off[n_frames] = (uint64_t)n_frames * codes_cap;
   }
-  const uint32_t e = tree_body<false>(hist + (uint64_t)f * kHistParts * 256, canon + (uint64_t)f * 256,
-                                      table + (uint64_t)f * 256, meta + (uint64_t)f * kMetaWords,
-                                      codes_len ? codes_len + f : nullptr, codes_cap, status ? status + f : nullptr,
-                                      nb * 64);
+  // the frame's symbol counts: the sum of its tile counts (wave w: tiles w, w + 16, ...,
+  // eight 8-byte loads in flight per lane, lane l: symbols 4l..4l+3), no global atomics
+  __shared__ uint32_t s_part[kCodeWaves][256], s_cnt[256];
+  {
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    const uint2 *th = reinterpret_cast<const uint2 *>(tile_hist + (uint64_t)f * ncode * 256);
+    uint32_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t t0 = wave; t0 < ncode; t0 += kCodeWaves * 8u) {
+      uint2 v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t t = t0 + kCodeWaves * k;
+        v[k] = t < ncode ? th[(uint64_t)t * 64 + lane] : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        acc[0] += v[k].x & 0xFFFFu;
+        acc[1] += v[k].x >> 16;
+        acc[2] += v[k].y & 0xFFFFu;
+        acc[3] += v[k].y >> 16;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) s_part[wave][4 * lane + j] = acc[j];
+    lds_barrier();
+    if (tid < 256) {
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kCodeWaves; ++w) c += s_part[w][tid];
+      s_cnt[tid] = c;
+    }
+    lds_barrier();
+  }
+  const uint32_t e = tree_body<false>(nullptr, canon + (uint64_t)f * 256, table + (uint64_t)f * 256,
+                                      meta + (uint64_t)f * kMetaWords, codes_len ? codes_len + f : nullptr,
+                                      codes_cap, status ? status + f : nullptr, nb * 64, s_cnt);
   if (tid >= 256) return;  // tree_body leaves the 256 symbol threads (4 waves)
   __shared__ uint32_t s_len[256], s_chunk[4 * kTileBatch];
   s_len[tid] = e & 0x1Fu;
-  __syncthreads();
+  lds_barrier();
   if (e & 0x80u) return;  // rejected frame (uniform): the pack kernel writes nothing
   // Tile offsets: wave w reduces tiles c + w * kTileBatch + [0, kTileBatch) of each chunk
   // of 4 * kTileBatch tiles (lane l: symbols 4l..4l+3 of a tile, one 8-byte load; all
@@ -1104,7 +1179,7 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
       x = wave_scan_dpp(x);
       if (lane == 63) s_chunk[wave * kTileBatch + k] = x;  // the tile's bits (< 2^21)
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
       // 4 * kTileBatch = 128 totals: two per lane
       const uint32_t a = s_chunk[2 * lane], b = s_chunk[2 * lane + 1];
@@ -1114,35 +1189,111 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
       if (c + 2 * lane + 1 < ncode) to[c + 2 * lane + 1] = base + a;
       carry += __builtin_amdgcn_readlane(incl, 63);
     }
-    __syncthreads();
+    lds_barrier();
   }
   if (tid == 0) to[ncode] = carry;
 }
 
+// Persistent packing: workgroup g packs the contiguous tiles [g * chunk, (g + 1) * chunk)
+// of all frames (tile i = tile i % ncode of frame i / ncode), one at a time; the next
+// tile's pixels, first bit and (on a frame change) code table word are in flight while
+// the current one is packed, so the per-tile chain is LDS and barriers, not HBM latency.
 __global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_pack_batch_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
-    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride) {
+    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total,
+    uint32_t chunk) {
   __shared__ uint32_t tab[256];
-  const uint32_t f = blockIdx.x / ncode, t = blockIdx.x - f * ncode;
-  if (!meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (status set by the tree)
   const uint32_t tid = threadIdx.x, part = tid & 7u;
-  const uint8_t *gray = px.gray + f * gray_stride;
-  const uint64_t b0 = (uint64_t)t * kCodeTile, b = b0 + (tid >> 3);
-  const bool on = b < nb;
-  const uint64_t gq = block_row(gray, px.W, px.H, px.bw, nb, px.vec, b, part);
-  const uint64_t gp = (t > 0 && tid < 8) ? block_row(gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
-  if (tid < 256) tab[tid] = table[(uint64_t)f * 256 + tid];
-  const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
-  uint32_t first_unused;
-  const uint64_t q = row_symbols(gq, part, px.delta, px.init_byte, &first_unused);
-  const uint64_t qp = row_symbols(gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // lanes 0-7 of wave 0
-  __syncthreads();  // tab
-  pack_emit(t, ncode, E, tab, q, qp, b, on, offsets + (uint64_t)f * nb,
-            reinterpret_cast<uint32_t *>(codes + f * codes_stride));
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(total, i0 + chunk);
+  if (i0 >= i1) return;  // workgroup-uniform
+  // iterators over (frame f, tile t) and the tile's first block (bx0, by0): no division
+  // per tile (a runtime divisor is a long scalar sequence)
+  uint32_t nf = i0 / ncode, nt = i0 - nf * ncode;
+  uint32_t nbx0 = (uint32_t)(((uint64_t)nt * kCodeTile) % px.bw), nby0 = (uint32_t)(((uint64_t)nt * kCodeTile) / px.bw);
+  const uint32_t k = tid >> 3;  // this lane's block in the tile
+  struct Next {
+    uint64_t gq, gp;
+    uint32_t E, tw, ok, f, t;
+  };
+  const auto fetch = [&]() {
+    Next n;
+    n.f = nf;
+    n.t = nt;
+    const uint8_t *gray = px.gray + nf * gray_stride;
+    const uint64_t b0 = (uint64_t)nt * kCodeTile, b = b0 + k;
+    if (px.vec) {
+      // unconditional 8-byte buffer loads (rows past the frame read as zero, out of
+      // range), so the prefetch is counted exactly in vmcnt
+      const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray, (uint64_t)px.W * px.H);
+      uint32_t bx = nbx0 + k, by = nby0;
+      if (px.bw >= kCodeTile) {
+        if (bx >= px.bw) {  // a tile spans at most two block rows
+          bx -= px.bw;
+          ++by;
+        }
+      } else {
+        by += bx / px.bw;
+        bx %= px.bw;
+      }
+      const uint32_t y = by * 8u + part;
+      const uint32_t oq = b < nb && y < px.H ? y * px.W + bx * 8u : kOob;
+      // lanes 0-7 (t > 0): row `tid` of the previous tile's last block
+      uint32_t px_ = nbx0, py_ = nby0;
+      if (px_ == 0) {
+        px_ = px.bw;
+        --py_;
+      }
+      const uint32_t yp = py_ * 8u + tid;
+      const uint32_t op = nt > 0 && tid < 8 && yp < px.H ? yp * px.W + (px_ - 1u) * 8u : kOob;
+      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+      const v2u32 vq = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)oq, 0, 0);
+      const v2u32 vp = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)op, 0, 0);
+      n.gq = ((uint64_t)vq.y << 32) | vq.x;
+      n.gp = ((uint64_t)vp.y << 32) | vp.x;
+    } else {
+      n.gq = block_row(gray, px.W, px.H, px.bw, nb, px.vec, b, part);
+      n.gp = (nt > 0 && tid < 8) ? block_row(gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
+    }
+    n.E = tile_off[(uint64_t)nf * (ncode + 1) + nt];
+    n.tw = tid < 256 ? table[(uint64_t)nf * 256 + tid] : 0u;
+    n.ok = (uint32_t)meta[(uint64_t)nf * kMetaWords + 1];
+    // advance to the next tile
+    if (++nt == ncode) {
+      nt = 0;
+      ++nf;
+      nbx0 = nby0 = 0;
+    } else {
+      nbx0 += kCodeTile;
+      while (nbx0 >= px.bw) {  // uniform; once per tile at most when bw >= 128
+        nbx0 -= px.bw;
+        ++nby0;
+      }
+    }
+    return n;
+  };
+  Next cur = fetch();
+  uint32_t tab_frame = 0xFFFFFFFFu;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const Next nx = i + 1 < i1 ? fetch() : cur;
+    const uint32_t f = cur.f, t = cur.t;
+    if (f != tab_frame) {  // workgroup-uniform; the previous tile's table reads are behind its barriers
+      if (tid < 256) tab[tid] = cur.tw;
+      lds_barrier();
+      tab_frame = f;
+    }
+    if (cur.ok) {  // a rejected frame (status set by the tree) writes nothing
+      const uint64_t b = (uint64_t)t * kCodeTile + k;
+      uint32_t first_unused;
+      const uint64_t q = row_symbols(cur.gq, part, px.delta, px.init_byte, &first_unused);
+      const uint64_t qp = row_symbols(cur.gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // lanes 0-7 of wave 0
+      pack_emit(t, ncode, cur.E, tab, q, qp, b, b < nb, offsets + (uint64_t)f * nb, nb,
+                reinterpret_cast<uint32_t *>(codes + f * codes_stride), codes_stride);
+    }
+    cur = nx;
+  }
 }
 
-struct BatchWorkspace {  // per-frame slices, each part 256-B aligned
-  uint64_t *hist;       // n x kHistParts x 256
+struct BatchWorkspace {  // per-frame slices, each part 256-B aligned; nothing needs zeroing
   uint32_t *table;      // n x 256
   uint64_t *meta;       // n x kMetaWords
   uint16_t *tile_hist;  // n x ncode x 256
@@ -1152,8 +1303,6 @@ struct BatchWorkspace {  // per-frame slices, each part 256-B aligned
 uint64_t carve_batch(uint8_t *base, uint64_t nb, uint32_t n, BatchWorkspace *w) {
   const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
   uint64_t o = 0;
-  if (w) w->hist = reinterpret_cast<uint64_t *>(base + o);
-  o += align256((uint64_t)n * kHistParts * 256 * 8);
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256((uint64_t)n * 256 * 4);
   if (w) w->meta = reinterpret_cast<uint64_t *>(base + o);
@@ -1322,21 +1471,27 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   BatchWorkspace w;
   carve_batch(static_cast<uint8_t *>(d_workspace), nb, n_frames, &w);
   hipStream_t s = (hipStream_t)stream;
-  // the trees re-zero the histograms they consumed; without the flag they are zeroed here
-  if (!(flags & MH_ENCODE_WORKSPACE_ZEROED) &&
-      hipMemsetAsync(w.hist, 0, (size_t)n_frames * kHistParts * 256 * 8, s) != hipSuccess)
-    return MH_ERR_HIP;
+  // every part of the workspace is written before it is read within the call (the tile
+  // counts by the split, the tables and tile offsets by the trees): nothing to clear
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
   const uint32_t nt = (uint32_t)(ncode * n_frames);
   hipLaunchKernelGGL(enc_split_kernel, dim3(nt), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
-                     nullptr, d_block_init, w.hist, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
-  hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(n_frames), dim3(kTreeThreads), 0, s, w.hist, d_canon_headers,
+                     nullptr, d_block_init, nullptr, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
+  hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(n_frames), dim3(kTreeThreads), 0, s, nullptr, d_canon_headers,
                      w.table, w.meta, d_codes_len, codes_frame_stride, d_status, nb, w.tile_hist, (uint32_t)ncode,
                      w.tile_off, d_frame_code_offsets, n_frames);
   const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
-  hipLaunchKernelGGL(enc_pack_batch_kernel, dim3(nt), dim3(kCodeThreads), 0, s, px, gray_frame_stride, nb,
-                     (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes, codes_frame_stride);
+  // persistent packing: two 1,024-thread workgroups per CU, contiguous tile chunks
+  int dev = -1, cus = 0;
+  if (!(s && hipStreamGetDevice(s, &dev) == hipSuccess) && hipGetDevice(&dev) != hipSuccess) return MH_ERR_HIP;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    return MH_ERR_HIP;
+  const uint32_t grid = std::min<uint32_t>(nt, 2u * (uint32_t)cus);
+  const uint32_t chunk = (nt + grid - 1) / grid;
+  hipLaunchKernelGGL(enc_pack_batch_kernel, dim3((nt + chunk - 1) / chunk), dim3(kCodeThreads), 0, s, px,
+                     gray_frame_stride, nb, (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes,
+                     codes_frame_stride, nt, chunk);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
