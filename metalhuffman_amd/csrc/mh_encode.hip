@@ -45,6 +45,9 @@ constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;  // a packer's wait limit: 1
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 constexpr uint32_t kFusedMaxTiles = 512;  // frames up to this many tiles take the two-kernel path
 
+#ifndef MH_SPLIT_RUNS  // A/B: merge runs of one symbol in a block row before the histogram atomics
+#define MH_SPLIT_RUNS 0
+#endif
 #ifndef MH_CODE_STAMPS  // diagnostic builds only: s_memrealtime phase stamps of enc_code_kernel
 #define MH_CODE_STAMPS 0
 #endif
@@ -117,6 +120,18 @@ constexpr uint32_t kHistCopies = 16;
 constexpr uint32_t kSplitBatch = 8;   // groups of 32 blocks whose rows a split workgroup loads at once
 constexpr uint32_t kSplitWgs = 256;   // split workgroups (four-kernel path): one global atomic per used bin each
 
+// Buffer descriptor from wave-uniform inputs (readfirstlane, so buffer ops need no
+// waterfall loop); offsets past `bytes` are dropped by the hardware.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t enc_rsrc(const void *base, uint64_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t n = (uint32_t)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
+constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past every descriptor's range: dropped
+
 // Row r (8 pixels, little-endian in a u64) of 8x8 block b, zero past the frame edge
 // (Util.m:256-318: zero-filled blocks, row-major inside a block).
 __device__ __forceinline__ uint64_t block_row(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw,
@@ -164,12 +179,53 @@ __device__ __forceinline__ uint64_t row_symbols(uint64_t q, uint32_t r, bool del
 // hist and tile_hist slices).
 constexpr uint32_t kTileGroups = kCodeTile / 32;
 static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgroup's batch covers a code tile");
+
+// Row r of this lane's block (32 g + lane / 8) of group g as ONE unconditional buffer
+// load (kVec: 8 bytes; else 8 byte loads), zero past the frame: a fixed count of loads
+// per lane, so several groups' loads stay in flight together (a load under a branch
+// makes the compiler wait for it at the join). The descriptor starts at the group's
+// first block row (uniform), so offsets stay 32-bit for any frame size.
+template <bool kVec>
+__device__ __forceinline__ uint64_t group_row(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw, uint64_t nb,
+                                              uint64_t g, uint32_t r) {
+  const uint32_t k = threadIdx.x >> 3;
+  const uint64_t gb = g * 32;
+  const uint32_t gb32 = (uint32_t)(gb < nb ? gb : nb);  // nb < 2^26
+  const uint32_t by0 = gb32 / bw;                       // uniform
+  uint32_t bx = gb32 - by0 * bw + k, by = by0;
+  if (bw >= 32) {
+    if (bx >= bw) {  // a group spans at most two block rows
+      bx -= bw;
+      ++by;
+    }
+  } else {
+    by += bx / bw;
+    bx %= bw;
+  }
+  const uint32_t y0 = by0 * 8u, y = by * 8u + r;
+  const bool in = gb + k < nb && y < H;
+  const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray + (uint64_t)y0 * W, y0 < H ? (uint64_t)(H - y0) * W : 0ull);
+  if constexpr (kVec) {
+    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+    const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)(in ? (y - y0) * W + bx * 8u : kOob), 0, 0);
+    return ((uint64_t)v.y << 32) | v.x;
+  } else {
+    uint64_t q = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 8; ++c)
+      q |= (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(rg, (int)(in && bx * 8u + c < W ? (y - y0) * W + bx * 8u + c : kOob),
+                                                         0, 0) << (8 * c);
+    return q;
+  }
+}
+
+template <bool kVec, bool kTiled>
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
-                                                        uint32_t vec, uint8_t *sym, uint8_t *block_init,
+                                                        uint8_t *sym, uint8_t *block_init,
                                                         uint64_t *hist, uint16_t *tile_hist, uint64_t *meta,
                                                         uint32_t ncode, uint64_t gray_stride) {
-  const bool tiled = tile_hist != nullptr;
+  constexpr bool tiled = kTiled;
   uint32_t wg = blockIdx.x;  // tiled: this frame's tile
   if (tiled) {
     const uint32_t f = blockIdx.x / ncode;
@@ -191,10 +247,8 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint32_t r = threadIdx.x & 7u;
   const uint32_t copy = threadIdx.x % kHistCopies;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
-  // one block row (8 pixels) of group g, zero past the frame edge
-  auto load_row = [&](uint64_t g) -> uint64_t {
-    return block_row(gray, W, H, bw, nb, vec, g * 32 + (threadIdx.x >> 3), r);
-  };
+  // block_init: buffer stores (a fixed count, lanes without a byte out of range)
+  const __amdgpu_buffer_rsrc_t rinit = enc_rsrc(block_init, block_init ? nb : 0ull);
   // one group of 32 blocks: deltas, init bytes, symbols out (four-kernel path; the
   // fused path's packer re-derives them from the pixels), histogram
   auto process = [&](uint64_t g, uint64_t q) {
@@ -202,10 +256,28 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     const bool on = b < nb;
     uint32_t first;
     const uint64_t v = row_symbols(q, r, delta, block_init != nullptr, &first);
-    if (block_init && r == 0 && on) block_init[b] = (uint8_t)first;
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && on ? (uint32_t)b : kOob), 0, 0);
     if (on) {
-      if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
+      if constexpr (!kTiled) {  // the four-kernel path's symbol buffer (large frames: 64-bit offsets)
+        if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
+      }
+#if MH_SPLIT_RUNS
+      // runs of one symbol in the row merged first: one atomic per run, not per symbol
+      uint32_t cur = (uint32_t)v & 0xFFu, n = 1;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) {
+        const uint32_t sj = (uint32_t)(v >> (8 * j)) & 0xFFu;
+        if (sj != cur) {
+          atomicAdd(&h[cur * kHistCopies + copy], n);
+          cur = sj;
+          n = 0;
+        }
+        ++n;
+      }
+      atomicAdd(&h[cur * kHistCopies + copy], n);
+#else
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+#endif
     }
   };
   // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
@@ -216,18 +288,18 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint64_t gfirst = tiled ? (uint64_t)wg * kTileGroups : blockIdx.x;
   const uint64_t gstride = tiled ? ngroups : (uint64_t)kSplitBatch * gridDim.x;
   for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
-    const uint32_t nu = tiled ? kTileGroups : kSplitBatch;
-    uint64_t q[kSplitBatch];
+    constexpr uint32_t nu = kTiled ? kTileGroups : kSplitBatch;
+    uint64_t q[nu];
 #pragma unroll
-    for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = u < nu ? load_row(g0 + u * ustep) : 0ull;
+    for (uint32_t u = 0; u < nu; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * ustep, r);
 #if MH_CODE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     MH_SPLIT_STAMP(1)
 #endif
 #pragma unroll
-    for (uint32_t u = 0; u < kSplitBatch; ++u) {
+    for (uint32_t u = 0; u < nu; ++u) {
       const uint64_t g = g0 + u * ustep;
-      if (u < nu && g < ngroups) process(g, q[u]);
+      if (g < ngroups) process(g, q[u]);
     }
   }
   MH_SPLIT_STAMP(2)
@@ -900,17 +972,6 @@ struct Pixels {  // the frame as the split reads it
 // computes those bits itself from that block's symbols and writes the word whole; a
 // tile leaves its own partial last word to the next tile (the last tile writes it and
 // the zero pad). Every code word is written exactly once: no clearing, no atomics.
-// Buffer descriptor from wave-uniform inputs (readfirstlane, so buffer ops need no
-// waterfall loop); offsets past `bytes` are dropped by the hardware.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t enc_rsrc(const void *base, uint64_t bytes) {
-  const uint64_t p = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  const uint32_t n = (uint32_t)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull);
-  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
-}
-constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past every descriptor's range: dropped
 
 // The stores are a fixed count of unconditional buffer stores per thread (lanes with
 // nothing to store use an out-of-range offset), so the compiler counts them exactly in
@@ -1194,102 +1255,164 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
   if (tid == 0) to[ncode] = carry;
 }
 
-// Persistent packing: workgroup g packs the contiguous tiles [g * chunk, (g + 1) * chunk)
-// of all frames (tile i = tile i % ncode of frame i / ncode), one at a time; the next
-// tile's pixels, first bit and (on a frame change) code table word are in flight while
-// the current one is packed, so the per-tile chain is LDS and barriers, not HBM latency.
-__global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_pack_batch_kernel(
+// Wave packing: each wave packs one tile alone, eight blocks per step (64 lanes, one
+// block row each), carrying its bit position from step to step in a register and the
+// step's last partial word in LDS: no workgroup barrier anywhere (a 1,024-thread
+// packer that shared a tile between 16 waves spent its time in the four workgroup
+// barriers per tile, profiles/r04_v4_encoder_batch_ab.txt). The next step's rows are
+// in flight while a step is packed (a fixed count of unconditional buffer loads).
+constexpr uint32_t kPackWaves = 4;     // waves per workgroup (independent of each other)
+constexpr uint32_t kStepSlots = 320;   // LDS words per wave: 5 per lane >= a step's 256 + the carry
+static_assert(kStepSlots >= 8 * 64 * 16 / 32 + 2, "a step's bits (<= 16-bit codes) plus the carry word");
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool kVec>
+__global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
-    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total,
-    uint32_t chunk) {
-  __shared__ uint32_t tab[256];
-  const uint32_t tid = threadIdx.x, part = tid & 7u;
-  const uint32_t i0 = blockIdx.x * chunk, i1 = min(total, i0 + chunk);
-  if (i0 >= i1) return;  // workgroup-uniform
-  // iterators over (frame f, tile t) and the tile's first block (bx0, by0): no division
-  // per tile (a runtime divisor is a long scalar sequence)
-  uint32_t nf = i0 / ncode, nt = i0 - nf * ncode;
-  uint32_t nbx0 = (uint32_t)(((uint64_t)nt * kCodeTile) % px.bw), nby0 = (uint32_t)(((uint64_t)nt * kCodeTile) / px.bw);
-  const uint32_t k = tid >> 3;  // this lane's block in the tile
-  struct Next {
-    uint64_t gq, gp;
-    uint32_t E, tw, ok, f, t;
-  };
-  const auto fetch = [&]() {
-    Next n;
-    n.f = nf;
-    n.t = nt;
-    const uint8_t *gray = px.gray + nf * gray_stride;
-    const uint64_t b0 = (uint64_t)nt * kCodeTile, b = b0 + k;
-    if (px.vec) {
-      // unconditional 8-byte buffer loads (rows past the frame read as zero, out of
-      // range), so the prefetch is counted exactly in vmcnt
-      const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray, (uint64_t)px.W * px.H);
-      uint32_t bx = nbx0 + k, by = nby0;
-      if (px.bw >= kCodeTile) {
-        if (bx >= px.bw) {  // a tile spans at most two block rows
-          bx -= px.bw;
-          ++by;
-        }
-      } else {
-        by += bx / px.bw;
-        bx %= px.bw;
+    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total) {
+  __shared__ uint32_t s_tab[kPackWaves][256];
+  __shared__ uint32_t s_w[kPackWaves][kStepSlots];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, k = lane >> 3, r = lane & 7u;
+  const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * kPackWaves + wave);
+  if (i >= total) return;  // wave-uniform; no workgroup barrier follows
+  const uint32_t f = i / ncode, t = i - f * ncode;
+  if (!(uint32_t)meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (the tree's status): nothing written
+  uint32_t *tab = s_tab[wave];
+  uint32_t *lw = s_w[wave];
+  reinterpret_cast<uint4 *>(tab)[lane] = reinterpret_cast<const uint4 *>(table + (uint64_t)f * 256)[lane];
+  const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
+  const uint8_t *gray = px.gray + f * gray_stride;
+  const uint64_t b0 = (uint64_t)t * kCodeTile;
+  const uint32_t nsteps = (uint32_t)((min<uint64_t>(kCodeTile, nb - b0) + 7) / 8);
+  const uint32_t by0 = (uint32_t)(b0 / px.bw), bx0 = (uint32_t)(b0 - (uint64_t)by0 * px.bw);
+  // one descriptor from the block row before the tile's first: 32-bit offsets for any frame
+  const uint32_t yb = by0 ? (by0 - 1u) * 8u : 0u;
+  const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray + (uint64_t)yb * px.W, (uint64_t)(px.H - yb) * px.W);
+  // row r of block (bx + k, by) wrapped into the frame, zero when !live or past the frame
+  const auto load_row = [&](uint32_t sbx, uint32_t sby, uint64_t sb, uint32_t kk, uint32_t rr, bool live) -> uint64_t {
+    uint32_t bx = sbx + kk, by = sby;
+    if (px.bw >= 8) {
+      if (bx >= px.bw) {
+        bx -= px.bw;
+        ++by;
       }
-      const uint32_t y = by * 8u + part;
-      const uint32_t oq = b < nb && y < px.H ? y * px.W + bx * 8u : kOob;
-      // lanes 0-7 (t > 0): row `tid` of the previous tile's last block
-      uint32_t px_ = nbx0, py_ = nby0;
-      if (px_ == 0) {
-        px_ = px.bw;
-        --py_;
-      }
-      const uint32_t yp = py_ * 8u + tid;
-      const uint32_t op = nt > 0 && tid < 8 && yp < px.H ? yp * px.W + (px_ - 1u) * 8u : kOob;
+    } else {
+      by += bx / px.bw;
+      bx %= px.bw;
+    }
+    const uint32_t y = by * 8u + rr;
+    const bool in = live && sb + kk < nb && y < px.H;
+    if constexpr (kVec) {
       typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-      const v2u32 vq = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)oq, 0, 0);
-      const v2u32 vp = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)op, 0, 0);
-      n.gq = ((uint64_t)vq.y << 32) | vq.x;
-      n.gp = ((uint64_t)vp.y << 32) | vp.x;
+      const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)(in ? (y - yb) * px.W + bx * 8u : kOob), 0, 0);
+      return ((uint64_t)v.y << 32) | v.x;
     } else {
-      n.gq = block_row(gray, px.W, px.H, px.bw, nb, px.vec, b, part);
-      n.gp = (nt > 0 && tid < 8) ? block_row(gray, px.W, px.H, px.bw, nb, px.vec, b0 - 1, tid) : 0ull;
+      uint64_t q = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < 8; ++c)
+        q |= (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(
+                 rg, (int)(in && bx * 8u + c < px.W ? (y - yb) * px.W + bx * 8u + c : kOob), 0, 0)
+             << (8 * c);
+      return q;
     }
-    n.E = tile_off[(uint64_t)nf * (ncode + 1) + nt];
-    n.tw = tid < 256 ? table[(uint64_t)nf * 256 + tid] : 0u;
-    n.ok = (uint32_t)meta[(uint64_t)nf * kMetaWords + 1];
-    // advance to the next tile
-    if (++nt == ncode) {
-      nt = 0;
-      ++nf;
-      nbx0 = nby0 = 0;
-    } else {
-      nbx0 += kCodeTile;
-      while (nbx0 >= px.bw) {  // uniform; once per tile at most when bw >= 128
-        nbx0 -= px.bw;
-        ++nby0;
-      }
-    }
-    return n;
   };
-  Next cur = fetch();
-  uint32_t tab_frame = 0xFFFFFFFFu;
-  for (uint32_t i = i0; i < i1; ++i) {
-    const Next nx = i + 1 < i1 ? fetch() : cur;
-    const uint32_t f = cur.f, t = cur.t;
-    if (f != tab_frame) {  // workgroup-uniform; the previous tile's table reads are behind its barriers
-      if (tid < 256) tab[tid] = cur.tw;
-      lds_barrier();
-      tab_frame = f;
+  uint32_t first_unused;
+  // the tile's first word starts with the previous block's last E % 32 bits: lanes 0-7
+  // recompute that block's codes (the previous tile leaves the shared word to this one)
+  uint32_t head = 0;
+  const uint32_t r0 = E & 31u;
+  if (r0) {  // wave-uniform; t > 0 here (tile 0 starts at bit 0)
+    const uint32_t pbx = bx0 ? bx0 - 1u : px.bw - 1u, pby = bx0 ? by0 : by0 - 1u;
+    const uint64_t qp = row_symbols(load_row(pbx, pby, b0 - 1, 0, lane, lane < 8), lane & 7u, px.delta, px.init_byte,
+                                    &first_unused);
+    uint32_t lenp = 0;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
+      const uint32_t len = e & 0xFFu;
+      acc = (acc << len) | ((e >> 16) >> (16 - len));  // the lane's codes MSB-first, last 64 bits
+      lenp += len;
     }
-    if (cur.ok) {  // a rejected frame (status set by the tree) writes nothing
-      const uint64_t b = (uint64_t)t * kCodeTile + k;
-      uint32_t first_unused;
-      const uint64_t q = row_symbols(cur.gq, part, px.delta, px.init_byte, &first_unused);
-      const uint64_t qp = row_symbols(cur.gp, tid & 7u, px.delta, px.init_byte, &first_unused);  // lanes 0-7 of wave 0
-      pack_emit(t, ncode, cur.E, tab, q, qp, b, b < nb, offsets + (uint64_t)f * nb, nb,
-                reinterpret_cast<uint32_t *>(codes + f * codes_stride), codes_stride);
+    if (lane >= 8) lenp = 0;
+    // bits of lanes after this one in the block; the lane's last bit lands at word bit
+    // 32 - r0 + after (bits before the word fall off the top)
+    const uint32_t incp = wave_scan_dpp(lenp);
+    const uint32_t after = __builtin_amdgcn_readlane(incp, 7) - incp;
+    uint32_t h = lane < 8 && after < r0 ? (uint32_t)(acc << (32u - r0 + after)) : 0u;
+    for (uint32_t o = 1; o < 8; o <<= 1) h |= __shfl_xor(h, o);
+    head = __builtin_amdgcn_readfirstlane(h);
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kStepSlots / 64; ++j) lw[lane + 64 * j] = lane + j == 0 ? bswap32(head) : 0u;
+  const __amdgpu_buffer_rsrc_t rw = enc_rsrc(codes + f * codes_stride, codes_stride);
+  const __amdgpu_buffer_rsrc_t ro = enc_rsrc(offsets + (uint64_t)f * nb, nb * 4u);
+  uint32_t pos = E;
+  uint32_t sbx = bx0, sby = by0;
+  uint64_t sb = b0;
+  uint64_t q = load_row(sbx, sby, sb, k, r, true);
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    // the next step's rows (a dead load past the tile's last step: fixed count)
+    uint32_t nbx = sbx + 8u, nby = sby;
+    while (nbx >= px.bw) {  // uniform; once per step at most when bw >= 8
+      nbx -= px.bw;
+      ++nby;
     }
-    cur = nx;
+    const uint64_t nq = load_row(nbx, nby, sb + 8, k, r, s + 1 < nsteps);
+    const bool on = sb + k < nb;
+    const uint64_t v = row_symbols(q, r, px.delta, px.init_byte, &first_unused);
+    uint64_t ch[2] = {0, 0};
+    uint32_t cl[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t e = tab[(uint32_t)(v >> (8 * j)) & 0xFFu];
+      const uint32_t len = e & 0xFFu;
+      ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
+      cl[j >> 2] += len;
+    }
+    const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
+    const uint32_t incl = wave_scan_dpp(nbits);
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63), pre = incl - nbits;
+    __builtin_amdgcn_raw_buffer_store_b32(pos + pre, ro, (int)(on && r == 0 ? (uint32_t)(sb + k) * 4u : kOob), 0, 0);
+    const uint32_t rr = pos & 31u;
+    if (on) {
+      or_bits(lw, rr + pre, ch[0], cl[0]);
+      or_bits(lw, rr + pre + cl[0], ch[1], cl[1]);
+    }
+    wave_sync();
+    // whole words out; the last partial word stays as the next step's first
+    const uint32_t nfull = (rr + T) >> 5, w0 = pos >> 5;
+    uint32_t wv[kStepSlots / 64];
+#pragma unroll
+    for (uint32_t j = 0; j < kStepSlots / 64; ++j) wv[j] = lw[lane + 64 * j];
+    const uint32_t carry = lw[nfull];
+#pragma unroll
+    for (uint32_t j = 0; j < kStepSlots / 64; ++j) {
+      const uint32_t w = lane + 64 * j;
+      __builtin_amdgcn_raw_buffer_store_b32(wv[j], rw, (int)(w < nfull ? (w0 + w) * 4u : kOob), 0, 0);
+    }
+    wave_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < kStepSlots / 64; ++j) lw[lane + 64 * j] = lane + j == 0 ? carry : 0u;
+    wave_sync();
+    pos += T;
+    q = nq;
+    sbx = nbx;
+    sby = nby;
+    sb += 8;
+  }
+  // the last tile writes its partial last word, then the zero pad up to the byte count
+  // rounded to words (the others leave that word to the next tile)
+  if (t + 1 == ncode) {
+    const uint32_t nw = (uint32_t)(((uint64_t)(pos + 7u) / 8u + MH_CODES_PAD + 3u) / 4u);
+    const uint32_t w = (pos >> 5) + lane;
+    const uint32_t val = lane == 0 ? lw[0] : 0u;
+    __builtin_amdgcn_raw_buffer_store_b32(val, rw, (int)(w < nw ? w * 4u : kOob), 0, 0);
   }
 }
 
@@ -1399,8 +1522,8 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   const int path = encode_kernels();
   if (ncode <= kFusedMaxTiles && path == 2) {
     // two launches: the tiled split, then tree + offsets + packing in one kernel
-    hipLaunchKernelGGL(enc_split_kernel, dim3((uint32_t)ncode), dim3(256), 0, s, d_gray, width, height, bw, nb,
-                       flags, vec, nullptr, d_block_init, w.hist, w.tile_hist, w.meta, (uint32_t)ncode, 0ull);
+    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3((uint32_t)ncode),
+                       dim3(256), 0, s, d_gray, width, height, bw, nb, flags, nullptr, d_block_init, w.hist, w.tile_hist, w.meta, (uint32_t)ncode, 0ull);
     const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
     hipLaunchKernelGGL(enc_code_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist,
                        d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, px, w.tile_hist, nb,
@@ -1408,8 +1531,8 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, kSplitWgs);
-  hipLaunchKernelGGL(enc_split_kernel, dim3(gsplit), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
-                     w.sym, d_block_init, w.hist, nullptr, w.meta, 0u, 0ull);
+  hipLaunchKernelGGL((vec ? enc_split_kernel<true, false> : enc_split_kernel<false, false>), dim3(gsplit), dim3(256), 0,
+                     s, d_gray, width, height, bw, nb, flags, w.sym, d_block_init, w.hist, nullptr, w.meta, 0u, 0ull);
   hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
                      d_codes_len, codes_cap, d_status, nb * 64);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
@@ -1476,22 +1599,15 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
   const uint32_t nt = (uint32_t)(ncode * n_frames);
-  hipLaunchKernelGGL(enc_split_kernel, dim3(nt), dim3(256), 0, s, d_gray, width, height, bw, nb, flags, vec,
-                     nullptr, d_block_init, nullptr, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
+  hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, s,
+                     d_gray, width, height, bw, nb, flags, nullptr, d_block_init, nullptr, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
   hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(n_frames), dim3(kTreeThreads), 0, s, nullptr, d_canon_headers,
                      w.table, w.meta, d_codes_len, codes_frame_stride, d_status, nb, w.tile_hist, (uint32_t)ncode,
                      w.tile_off, d_frame_code_offsets, n_frames);
   const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
-  // persistent packing: two 1,024-thread workgroups per CU, contiguous tile chunks
-  int dev = -1, cus = 0;
-  if (!(s && hipStreamGetDevice(s, &dev) == hipSuccess) && hipGetDevice(&dev) != hipSuccess) return MH_ERR_HIP;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-    return MH_ERR_HIP;
-  const uint32_t grid = std::min<uint32_t>(nt, 2u * (uint32_t)cus);
-  const uint32_t chunk = (nt + grid - 1) / grid;
-  hipLaunchKernelGGL(enc_pack_batch_kernel, dim3((nt + chunk - 1) / chunk), dim3(kCodeThreads), 0, s, px,
-                     gray_frame_stride, nb, (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes,
-                     codes_frame_stride, nt, chunk);
+  hipLaunchKernelGGL(vec ? enc_pack_wave_kernel<true> : enc_pack_wave_kernel<false>,
+                     dim3((nt + kPackWaves - 1) / kPackWaves), dim3(kPackWaves * 64), 0, s, px, gray_frame_stride, nb,
+                     (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes, codes_frame_stride, nt);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 

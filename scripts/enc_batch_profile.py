@@ -30,6 +30,7 @@ for f in (0, n - 1):
     ref = mh.encode_frame(imgs[f])
     assert np.array_equal(a.frame(f).codes.cpu().numpy(), ref.codes), f
 alg = bb.size + ref.codes.size + 4 * ref.n_blocks  # pixels in, codes + offsets out
+print(f"alg_bytes {alg * n} per call of {n} frames")
 for rep in range(3):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()

@@ -1,9 +1,15 @@
-# Round-4 GPU check: parity tests, smoke, the driver's bench command, a rocprofv3 kernel
+# Round-4 GPU check: a full rebuild on the box, parity tests, smoke, the driver's bench command, a rocprofv3 kernel
 # trace of the headline workload, the batched encoder and the multi-GPU C host (fail-fast).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the library the tests load is compiled and linked HERE, on the box,
+# from this snapshot's sources (--force: every object and the link), not the pushed one
+sha256sum metalhuffman_amd/libmetalhuffman_amd.so > gpurun_out/build_on_box.log
+timeout -k 10 900 python -m metalhuffman_amd.build --force >> gpurun_out/build_on_box.log 2>&1 || { tail -20 gpurun_out/build_on_box.log; exit 1; }
+sha256sum metalhuffman_amd/libmetalhuffman_amd.so >> gpurun_out/build_on_box.log
+grep -c -- "--offload-arch=gfx950" gpurun_out/build_on_box.log; tail -1 gpurun_out/build_on_box.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log; grep -c PASSED gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
