@@ -219,6 +219,52 @@ __device__ __forceinline__ uint64_t group_row(const uint8_t *gray, uint32_t W, u
   }
 }
 
+// The tiled split's rows: lane k's blocks tb + k + 32 u (u < N) of the tile starting at
+// block tb, row r, from one descriptor at the tile's first block row. The tile's
+// coordinates are uniform (one scalar division); a lane's block wraps into the next
+// block row at most once when the frame is >= kCodeTile blocks wide.
+template <bool kVec, uint32_t N>
+__device__ __forceinline__ void tile_rows(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw, uint64_t nb,
+                                          uint32_t tb, uint32_t r, uint64_t (&q)[N]) {
+  // no 64-bit compares and no per-load v_mul_lo (quarter rate): 32-bit block indices
+  // (nb < 2^26), the row offset r * W once, a wrapped block adds 8 W
+  const uint32_t k = threadIdx.x >> 3, nb32 = (uint32_t)nb;
+  const uint32_t tby = tb / bw, tbx = tb - tby * bw;
+  const uint32_t y0 = tby * 8u, hrem = H - y0, w8 = 8u * W;
+  const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray + (uint64_t)y0 * W, (uint64_t)hrem * W);
+  uint32_t rowoff = r * W;
+  asm volatile("" : "+v"(rowoff));  // kept as is (else folded back into (dy + r) * W per load)
+#pragma unroll
+  for (uint32_t u = 0; u < N; ++u) {
+    uint32_t bx = tbx + k + 32u * u, dy = 0, doff = 0;
+    if (bw >= kCodeTile) {
+      const bool wrap = bx >= bw;
+      bx = wrap ? bx - bw : bx;
+      dy = wrap ? 8u : 0u;
+      doff = wrap ? w8 : 0u;
+    } else {
+      const uint32_t d = bx / bw;
+      bx -= d * bw;
+      dy = d * 8u;
+      doff = dy * W;
+    }
+    const bool in = tb + k + 32u * u < nb32 && dy + r < hrem;
+    const uint32_t off = doff + rowoff + bx * 8u;
+    if constexpr (kVec) {
+      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+      const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)(in ? off : kOob), 0, 0);
+      q[u] = ((uint64_t)v.y << 32) | v.x;
+    } else {
+      uint64_t x = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < 8; ++c)
+        x |= (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(rg, (int)(in && bx * 8u + c < W ? off + c : kOob), 0, 0)
+             << (8 * c);
+      q[u] = x;
+    }
+  }
+}
+
 template <bool kVec, bool kTiled>
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
@@ -242,8 +288,14 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   }
   MH_SPLIT_STAMP(0)
   __shared__ uint32_t h[256 * kHistCopies];
-  for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
-  lds_barrier();
+  // the histogram is cleared behind the first batch's loads (their HBM round trip
+  // covers it), before any atomic
+  bool cleared = false;
+  const auto clear_hist = [&]() {
+    for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
+    lds_barrier();
+    cleared = true;
+  };
   const uint32_t r = threadIdx.x & 7u;
   const uint32_t copy = threadIdx.x % kHistCopies;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
@@ -290,8 +342,13 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
     constexpr uint32_t nu = kTiled ? kTileGroups : kSplitBatch;
     uint64_t q[nu];
+    if constexpr (kTiled) {
+      tile_rows<kVec>(gray, W, H, bw, nb, (uint32_t)g0 * 32u, r, q);
+    } else {
 #pragma unroll
-    for (uint32_t u = 0; u < nu; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * ustep, r);
+      for (uint32_t u = 0; u < nu; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * ustep, r);
+    }
+    if (!cleared) clear_hist();  // workgroup-uniform
 #if MH_CODE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     MH_SPLIT_STAMP(1)
@@ -303,6 +360,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     }
   }
   MH_SPLIT_STAMP(2)
+  if (!cleared) clear_hist();  // no group at all
   lds_barrier();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
@@ -1173,11 +1231,13 @@ constexpr uint32_t kTileBatch = 32;  // tiles per wave and chunk of the tile-off
 __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
     uint64_t *hist, uint8_t *canon, uint32_t *table, uint64_t *meta, uint64_t *codes_len, uint64_t codes_cap,
     int32_t *status, uint64_t nb, const uint16_t *tile_hist, uint32_t ncode, uint32_t *tile_off,
-    uint64_t *frame_off, uint32_t n_frames) {
+    uint64_t *frame_off, uint32_t f0, uint32_t n_frames) {
+  // f0: this launch's first frame of the call (its pointers start there; frame_off is
+  // the call's, indexed by call frame)
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
   if (frame_off && tid == 0) {  // optional: the decoder's frame_code_offsets for fixed slots
-    frame_off[f] = (uint64_t)f * codes_cap;
-    if (f + 1 == n_frames) frame_off[n_frames] = (uint64_t)n_frames * codes_cap;
+    frame_off[f0 + f] = (uint64_t)(f0 + f) * codes_cap;
+    if (f0 + f + 1 == n_frames) frame_off[n_frames] = (uint64_t)n_frames * codes_cap;
   }
   // the frame's symbol counts: the sum of its tile counts (wave w: tiles w, w + 16, ...,
   // eight 8-byte loads in flight per lane, lane l: symbols 4l..4l+3), no global atomics
@@ -1262,7 +1322,7 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
 // barriers per tile, profiles/r04_v4_encoder_batch_ab.txt). The next step's rows are
 // in flight while a step is packed (a fixed count of unconditional buffer loads).
 constexpr uint32_t kPackWaves = 4;     // waves per workgroup (independent of each other)
-constexpr uint32_t kStepSlots = 320;   // LDS words per wave: 5 per lane >= a step's 256 + the carry
+constexpr uint32_t kStepSlots = 272;   // LDS words per wave (68 quads): a step's <= 257 words + or_bits' reach
 static_assert(kStepSlots >= 8 * 64 * 16 / 32 + 2, "a step's bits (<= 16-bit codes) plus the carry word");
 
 __device__ __forceinline__ void wave_sync() {
@@ -1276,7 +1336,7 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
     const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total) {
   __shared__ uint32_t s_tab[kPackWaves][256];
-  __shared__ uint32_t s_w[kPackWaves][kStepSlots];
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[kPackWaves][kStepSlots];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, k = lane >> 3, r = lane & 7u;
   const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * kPackWaves + wave);
   if (i >= total) return;  // wave-uniform; no workgroup barrier follows
@@ -1284,7 +1344,20 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   if (!(uint32_t)meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (the tree's status): nothing written
   uint32_t *tab = s_tab[wave];
   uint32_t *lw = s_w[wave];
-  reinterpret_cast<uint4 *>(tab)[lane] = reinterpret_cast<const uint4 *>(table + (uint64_t)f * 256)[lane];
+  {
+    // the frame's table as len << 16 | right-aligned code (the tree's words hold the
+    // code left-aligned in 16 bits): two symbols' codes combine in one v_lshl_or
+    uint4 v = reinterpret_cast<const uint4 *>(table + (uint64_t)f * 256)[lane];
+    const auto ra = [](uint32_t e) {
+      const uint32_t L = e & 0x1Fu;
+      return L ? (L << 16) | ((e >> 16) >> (16u - L)) : 0u;
+    };
+    v.x = ra(v.x);
+    v.y = ra(v.y);
+    v.z = ra(v.z);
+    v.w = ra(v.w);
+    reinterpret_cast<uint4 *>(tab)[lane] = v;
+  }
   const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
   const uint8_t *gray = px.gray + f * gray_stride;
   const uint64_t b0 = (uint64_t)t * kCodeTile;
@@ -1294,29 +1367,35 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   const uint32_t yb = by0 ? (by0 - 1u) * 8u : 0u;
   const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray + (uint64_t)yb * px.W, (uint64_t)(px.H - yb) * px.W);
   // row r of block (bx + k, by) wrapped into the frame, zero when !live or past the frame
-  const auto load_row = [&](uint32_t sbx, uint32_t sby, uint64_t sb, uint32_t kk, uint32_t rr, bool live) -> uint64_t {
-    uint32_t bx = sbx + kk, by = sby;
+  // (32-bit block indices, nb < 2^26; the step's row offset uniform, r * W per lane
+  // once, a wrapped block adds 8 W: no per-step v_mul_lo, which is quarter rate)
+  const uint32_t nb32 = (uint32_t)nb, w8 = 8u * px.W;
+  const auto load_row = [&](uint32_t sbx, uint32_t sby, uint32_t sb, uint32_t kk, uint32_t rr, uint32_t rrW,
+                            bool live) -> uint64_t {
+    uint32_t bx = sbx + kk, dy = 0, doff = 0;
     if (px.bw >= 8) {
-      if (bx >= px.bw) {
-        bx -= px.bw;
-        ++by;
-      }
+      const bool wrap = bx >= px.bw;
+      bx = wrap ? bx - px.bw : bx;
+      dy = wrap ? 8u : 0u;
+      doff = wrap ? w8 : 0u;
     } else {
-      by += bx / px.bw;
-      bx %= px.bw;
+      const uint32_t d = bx / px.bw;
+      bx -= d * px.bw;
+      dy = d * 8u;
+      doff = dy * px.W;
     }
-    const uint32_t y = by * 8u + rr;
-    const bool in = live && sb + kk < nb && y < px.H;
+    const uint32_t ys = sby * 8u - yb;  // uniform: the step's first block row in the descriptor
+    const bool in = live && sb + kk < nb32 && ys + dy + rr < px.H - yb;
+    const uint32_t off = ys * px.W + doff + rrW + bx * 8u;
     if constexpr (kVec) {
       typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-      const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)(in ? (y - yb) * px.W + bx * 8u : kOob), 0, 0);
+      const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)(in ? off : kOob), 0, 0);
       return ((uint64_t)v.y << 32) | v.x;
     } else {
       uint64_t q = 0;
 #pragma unroll
       for (uint32_t c = 0; c < 8; ++c)
-        q |= (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(
-                 rg, (int)(in && bx * 8u + c < px.W ? (y - yb) * px.W + bx * 8u + c : kOob), 0, 0)
+        q |= (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(rg, (int)(in && bx * 8u + c < px.W ? off + c : kOob), 0, 0)
              << (8 * c);
       return q;
     }
@@ -1328,15 +1407,16 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   const uint32_t r0 = E & 31u;
   if (r0) {  // wave-uniform; t > 0 here (tile 0 starts at bit 0)
     const uint32_t pbx = bx0 ? bx0 - 1u : px.bw - 1u, pby = bx0 ? by0 : by0 - 1u;
-    const uint64_t qp = row_symbols(load_row(pbx, pby, b0 - 1, 0, lane, lane < 8), lane & 7u, px.delta, px.init_byte,
+    const uint64_t qp = row_symbols(load_row(pbx, pby, (uint32_t)b0 - 1u, 0, lane, lane * px.W, lane < 8), lane & 7u,
+                                    px.delta, px.init_byte,
                                     &first_unused);
     uint32_t lenp = 0;
     uint64_t acc = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t e = tab[(uint32_t)(qp >> (8 * j)) & 0xFFu];
-      const uint32_t len = e & 0xFFu;
-      acc = (acc << len) | ((e >> 16) >> (16 - len));  // the lane's codes MSB-first, last 64 bits
+      const uint32_t len = e >> 16;
+      acc = (acc << len) | (e & 0xFFFFu);  // the lane's codes MSB-first, last 64 bits
       lenp += len;
     }
     if (lane >= 8) lenp = 0;
@@ -1348,14 +1428,22 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     for (uint32_t o = 1; o < 8; o <<= 1) h |= __shfl_xor(h, o);
     head = __builtin_amdgcn_readfirstlane(h);
   }
-#pragma unroll
-  for (uint32_t j = 0; j < kStepSlots / 64; ++j) lw[lane + 64 * j] = lane + j == 0 ? bswap32(head) : 0u;
+  typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+  v4u32 *lq = reinterpret_cast<v4u32 *>(lw);
+  // the step's words as quads: one 16-B LDS write / read and one 16-B store per lane
+  const auto clear_words = [&](uint32_t first) {
+    lq[lane] = v4u32{lane == 0 ? first : 0u, 0u, 0u, 0u};
+    if (lane < kStepSlots / 4 - 64) lq[64 + lane] = v4u32{0u, 0u, 0u, 0u};
+  };
+  clear_words(bswap32(head));
   const __amdgpu_buffer_rsrc_t rw = enc_rsrc(codes + f * codes_stride, codes_stride);
   const __amdgpu_buffer_rsrc_t ro = enc_rsrc(offsets + (uint64_t)f * nb, nb * 4u);
   uint32_t pos = E;
   uint32_t sbx = bx0, sby = by0;
-  uint64_t sb = b0;
-  uint64_t q = load_row(sbx, sby, sb, k, r, true);
+  uint32_t sb = (uint32_t)b0;
+  uint32_t rW = r * px.W;
+  asm volatile("" : "+v"(rW));  // kept as is (else folded back into (ys + r) * W per step)
+  uint64_t q = load_row(sbx, sby, sb, k, r, rW, true);
   for (uint32_t s = 0; s < nsteps; ++s) {
     // the next step's rows (a dead load past the tile's last step: fixed count)
     uint32_t nbx = sbx + 8u, nby = sby;
@@ -1363,22 +1451,24 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
       nbx -= px.bw;
       ++nby;
     }
-    const uint64_t nq = load_row(nbx, nby, sb + 8, k, r, s + 1 < nsteps);
-    const bool on = sb + k < nb;
+    const uint64_t nq = load_row(nbx, nby, sb + 8u, k, r, rW, s + 1 < nsteps);
+    const bool on = sb + k < nb32;
     const uint64_t v = row_symbols(q, r, px.delta, px.init_byte, &first_unused);
-    uint64_t ch[2] = {0, 0};
-    uint32_t cl[2] = {0, 0};
+    // codes MSB-first: pairs in 32 bits (v_lshl_or), then two chunks of four in 64
+    uint32_t pc[4], pl[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t e = tab[(uint32_t)(v >> (8 * j)) & 0xFFu];
-      const uint32_t len = e & 0xFFu;
-      ch[j >> 2] = (ch[j >> 2] << len) | ((e >> 16) >> (16 - len));
-      cl[j >> 2] += len;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t e0 = tab[(uint32_t)(v >> (16 * j)) & 0xFFu], e1 = tab[(uint32_t)(v >> (16 * j + 8)) & 0xFFu];
+      const uint32_t l1 = e1 >> 16;
+      pc[j] = ((e0 & 0xFFFFu) << l1) | (e1 & 0xFFFFu);
+      pl[j] = (e0 >> 16) + l1;
     }
+    const uint64_t ch[2] = {((uint64_t)pc[0] << pl[1]) | pc[1], ((uint64_t)pc[2] << pl[3]) | pc[3]};
+    const uint32_t cl[2] = {pl[0] + pl[1], pl[2] + pl[3]};
     const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
     const uint32_t incl = wave_scan_dpp(nbits);
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63), pre = incl - nbits;
-    __builtin_amdgcn_raw_buffer_store_b32(pos + pre, ro, (int)(on && r == 0 ? (uint32_t)(sb + k) * 4u : kOob), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(pos + pre, ro, (int)(on && r == 0 ? (sb + k) * 4u : kOob), 0, 0);
     const uint32_t rr = pos & 31u;
     if (on) {
       or_bits(lw, rr + pre, ch[0], cl[0]);
@@ -1386,19 +1476,15 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     }
     wave_sync();
     // whole words out; the last partial word stays as the next step's first
-    const uint32_t nfull = (rr + T) >> 5, w0 = pos >> 5;
-    uint32_t wv[kStepSlots / 64];
-#pragma unroll
-    for (uint32_t j = 0; j < kStepSlots / 64; ++j) wv[j] = lw[lane + 64 * j];
+    const uint32_t nfull = (rr + T) >> 5, w0 = pos >> 5, nq4 = nfull >> 2;
+    const v4u32 quad = lq[lane];                                   // words 4 lane .. 4 lane + 3
+    const uint32_t tail = lw[min(4u * nq4 + lane, kStepSlots - 1u)];  // lanes < nfull % 4: the last words
     const uint32_t carry = lw[nfull];
-#pragma unroll
-    for (uint32_t j = 0; j < kStepSlots / 64; ++j) {
-      const uint32_t w = lane + 64 * j;
-      __builtin_amdgcn_raw_buffer_store_b32(wv[j], rw, (int)(w < nfull ? (w0 + w) * 4u : kOob), 0, 0);
-    }
+    __builtin_amdgcn_raw_buffer_store_b128(quad, rw, (int)(lane < nq4 ? (w0 + 4u * lane) * 4u : kOob), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(tail, rw, (int)(lane < (nfull & 3u) ? (w0 + 4u * nq4 + lane) * 4u : kOob), 0,
+                                          0);
     wave_sync();
-#pragma unroll
-    for (uint32_t j = 0; j < kStepSlots / 64; ++j) lw[lane + 64 * j] = lane + j == 0 ? carry : 0u;
+    clear_words(carry);
     wave_sync();
     pos += T;
     q = nq;
@@ -1598,16 +1684,34 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   // counts by the split, the tables and tile offsets by the trees): nothing to clear
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
-  const uint32_t nt = (uint32_t)(ncode * n_frames);
-  hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, s,
-                     d_gray, width, height, bw, nb, flags, nullptr, d_block_init, nullptr, w.tile_hist, nullptr, (uint32_t)ncode, gray_frame_stride);
-  hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(n_frames), dim3(kTreeThreads), 0, s, nullptr, d_canon_headers,
-                     w.table, w.meta, d_codes_len, codes_frame_stride, d_status, nb, w.tile_hist, (uint32_t)ncode,
-                     w.tile_off, d_frame_code_offsets, n_frames);
-  const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
-  hipLaunchKernelGGL(vec ? enc_pack_wave_kernel<true> : enc_pack_wave_kernel<false>,
-                     dim3((nt + kPackWaves - 1) / kPackWaves), dim3(kPackWaves * 64), 0, s, px, gray_frame_stride, nb,
-                     (uint32_t)ncode, w.table, w.meta, w.tile_off, d_block_offsets, d_codes, codes_frame_stride, nt);
+  const Pixels px0{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
+  // frames [f0, f0 + m): split, trees, packing on stream st
+  const auto sub_batch = [&](hipStream_t st, uint32_t f0, uint32_t m) {
+    const uint32_t nt = (uint32_t)(ncode * m);
+    const uint8_t *gray = d_gray + f0 * gray_frame_stride;
+    uint8_t *binit = d_block_init ? d_block_init + (uint64_t)f0 * nb : nullptr;
+    uint16_t *th = w.tile_hist + (uint64_t)f0 * ncode * 256;
+    uint32_t *table = w.table + (uint64_t)f0 * 256;
+    uint64_t *meta = w.meta + (uint64_t)f0 * kMetaWords;
+    uint32_t *to = w.tile_off + (uint64_t)f0 * (ncode + 1);
+    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, st,
+                       gray, width, height, bw, nb, flags, nullptr, binit, nullptr, th, nullptr, (uint32_t)ncode,
+                       gray_frame_stride);
+    hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(m), dim3(kTreeThreads), 0, st, nullptr,
+                       d_canon_headers + (uint64_t)f0 * 256, table, meta, d_codes_len ? d_codes_len + f0 : nullptr,
+                       codes_frame_stride, d_status ? d_status + f0 : nullptr, nb, th, (uint32_t)ncode, to,
+                       d_frame_code_offsets, f0, n_frames);
+    Pixels px = px0;
+    px.gray = gray;
+    hipLaunchKernelGGL(vec ? enc_pack_wave_kernel<true> : enc_pack_wave_kernel<false>,
+                       dim3((nt + kPackWaves - 1) / kPackWaves), dim3(kPackWaves * 64), 0, st, px, gray_frame_stride, nb,
+                       (uint32_t)ncode, table, meta, to, d_block_offsets + (uint64_t)f0 * nb,
+                       d_codes + f0 * codes_frame_stride, codes_frame_stride, nt);
+  };
+  // One sub-batch: splitting the call into sub-batches alternated over a second stream
+  // (trees beside another sub-batch's split / packing) measured slower, and the packer's
+  // pixel re-reads did not drop (profiles/r04_v4_encoder_batch_ab.txt).
+  sub_batch(s, 0, n_frames);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 

@@ -5,16 +5,23 @@ bytes (pixels in, codes + block offsets out).
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are
 KiB; FETCH_SIZE reports half the bytes of wide coalesced streaming reads (x2).
 
-    python scripts/enc_batch_pmc.py DIR [DIR ...] [--alg BYTES]
+    python scripts/enc_batch_pmc.py DIR [DIR ...] [--alg BYTES] [--calls N]
+
+Values are per CALL (all of a call's dispatches of a kernel summed: a call may launch
+each kernel once per sub-batch); enc_batch_profile.py 64 2 makes 7 calls.
 """
 import csv
 import glob
 import os
-import statistics
 import sys
 
 args = sys.argv[1:]
 alg = None
+calls = 7
+if "--calls" in args:
+    i = args.index("--calls")
+    calls = int(args[i + 1])
+    del args[i:i + 2]
 if "--alg" in args:
     i = args.index("--alg")
     alg = float(args[i + 1])
@@ -30,10 +37,10 @@ for d in args:
                     vals[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 tot = {}
 for k, cs in vals.items():
-    print(f"== {k} (per dispatch)")
+    print(f"== {k} (per call of the batch: sum over its dispatches)")
     for c, per in sorted(cs.items()):
-        m = statistics.mean(per.values())
-        print(f"  {c:24s} n={len(per):3d} mean={m:.4e}")
+        m = sum(per.values()) / calls
+        print(f"  {c:24s} dispatches={len(per):3d} per_call={m:.4e}")
         if c in ("FETCH_SIZE", "WRITE_SIZE"):
             tot[c] = tot.get(c, 0.0) + m * 1024.0 * (2.0 if c == "FETCH_SIZE" else 1.0)
 if tot:
