@@ -1315,15 +1315,18 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
   if (tid == 0) to[ncode] = carry;
 }
 
-// Wave packing: each wave packs one tile alone, eight blocks per step (64 lanes, one
-// block row each), carrying its bit position from step to step in a register and the
-// step's last partial word in LDS: no workgroup barrier anywhere (a 1,024-thread
+// Wave packing: each wave packs one tile alone, sixteen blocks per step (64 lanes: lane
+// 8 m + r holds row r of the step's blocks 2 m and 2 m + 1, one 16-byte load when the
+// pair shares a block row), carrying its bit position from step to step in a register
+// and the step's last partial word in LDS: no workgroup barrier anywhere (a 1,024-thread
 // packer that shared a tile between 16 waves spent its time in the four workgroup
-// barriers per tile, profiles/r04_v4_encoder_batch_ab.txt). The next step's rows are
-// in flight while a step is packed (a fixed count of unconditional buffer loads).
+// barriers per tile, profiles/r04_v4_encoder_batch_ab.txt). The next step's rows are in
+// flight while a step is packed (a fixed count of unconditional buffer loads).
 constexpr uint32_t kPackWaves = 4;     // waves per workgroup (independent of each other)
-constexpr uint32_t kStepSlots = 272;   // LDS words per wave (68 quads): a step's <= 257 words + or_bits' reach
-static_assert(kStepSlots >= 8 * 64 * 16 / 32 + 2, "a step's bits (<= 16-bit codes) plus the carry word");
+constexpr uint32_t kStepBlocks = 16;
+constexpr uint32_t kStepSlots = 528;   // LDS words per wave (132 quads): a step's <= 513 words + or_bits' reach
+static_assert(kStepSlots >= kStepBlocks * 64 * 16 / 32 + 4 && kStepSlots % 4 == 0 && kStepSlots / 4 - 128 <= 64,
+              "a step's bits (<= 16-bit codes), the carry word and or_bits' reach");
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1331,7 +1334,9 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool kVec>
+// kPair: 8-byte aligned rows and an even frame width in blocks (a pair never straddles
+// a block row): one 16-byte load per lane and step
+template <bool kVec, bool kPair>
 __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
     const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total) {
@@ -1361,7 +1366,7 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
   const uint8_t *gray = px.gray + f * gray_stride;
   const uint64_t b0 = (uint64_t)t * kCodeTile;
-  const uint32_t nsteps = (uint32_t)((min<uint64_t>(kCodeTile, nb - b0) + 7) / 8);
+  const uint32_t nsteps = (uint32_t)((min<uint64_t>(kCodeTile, nb - b0) + kStepBlocks - 1) / kStepBlocks);
   const uint32_t by0 = (uint32_t)(b0 / px.bw), bx0 = (uint32_t)(b0 - (uint64_t)by0 * px.bw);
   // one descriptor from the block row before the tile's first: 32-bit offsets for any frame
   const uint32_t yb = by0 ? (by0 - 1u) * 8u : 0u;
@@ -1373,7 +1378,7 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   const auto load_row = [&](uint32_t sbx, uint32_t sby, uint32_t sb, uint32_t kk, uint32_t rr, uint32_t rrW,
                             bool live) -> uint64_t {
     uint32_t bx = sbx + kk, dy = 0, doff = 0;
-    if (px.bw >= 8) {
+    if (px.bw >= kStepBlocks) {  // kk < kStepBlocks: one wrap at most
       const bool wrap = bx >= px.bw;
       bx = wrap ? bx - px.bw : bx;
       dy = wrap ? 8u : 0u;
@@ -1433,7 +1438,8 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   // the step's words as quads: one 16-B LDS write / read and one 16-B store per lane
   const auto clear_words = [&](uint32_t first) {
     lq[lane] = v4u32{lane == 0 ? first : 0u, 0u, 0u, 0u};
-    if (lane < kStepSlots / 4 - 64) lq[64 + lane] = v4u32{0u, 0u, 0u, 0u};
+    lq[64 + lane] = v4u32{0u, 0u, 0u, 0u};
+    if (lane < kStepSlots / 4 - 128) lq[128 + lane] = v4u32{0u, 0u, 0u, 0u};
   };
   clear_words(bswap32(head));
   const __amdgpu_buffer_rsrc_t rw = enc_rsrc(codes + f * codes_stride, codes_stride);
@@ -1443,54 +1449,108 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   uint32_t sb = (uint32_t)b0;
   uint32_t rW = r * px.W;
   asm volatile("" : "+v"(rW));  // kept as is (else folded back into (ys + r) * W per step)
-  uint64_t q = load_row(sbx, sby, sb, k, r, rW, true);
+  // row r of the pair (2 k, 2 k + 1) of the step starting at block (sbx, sby) = sb
+  const auto load_pair = [&](uint32_t bx_, uint32_t by_, uint32_t sb_, bool live, uint64_t &qa, uint64_t &qb) {
+    if constexpr (kPair) {
+      uint32_t bx = bx_ + 2u * k, doff = 0, dy = 0;
+      if (px.bw >= kStepBlocks) {
+        const bool wrap = bx >= px.bw;
+        bx = wrap ? bx - px.bw : bx;
+        dy = wrap ? 8u : 0u;
+        doff = wrap ? w8 : 0u;
+      } else {
+        const uint32_t d = bx / px.bw;
+        bx -= d * px.bw;
+        dy = d * 8u;
+        doff = dy * px.W;
+      }
+      const uint32_t ys = by_ * 8u - yb;
+      const bool in = live && sb_ + 2u * k < nb32 && ys + dy + r < px.H - yb;
+      // both blocks are inside the frame when the first is (an even width, an even first block)
+      const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(in ? ys * px.W + doff + rW + bx * 8u : kOob), 0, 0);
+      qa = ((uint64_t)v.y << 32) | v.x;
+      qb = ((uint64_t)v.w << 32) | v.z;
+    } else {
+      qa = load_row(bx_, by_, sb_, 2u * k, r, rW, live);
+      qb = load_row(bx_, by_, sb_, 2u * k + 1u, r, rW, live);
+    }
+  };
+  uint64_t qa, qb;
+  load_pair(sbx, sby, sb, true, qa, qb);
   for (uint32_t s = 0; s < nsteps; ++s) {
     // the next step's rows (a dead load past the tile's last step: fixed count)
-    uint32_t nbx = sbx + 8u, nby = sby;
-    while (nbx >= px.bw) {  // uniform; once per step at most when bw >= 8
+    uint32_t nbx = sbx + kStepBlocks, nby = sby;
+    while (nbx >= px.bw) {  // uniform; once per step at most when bw >= kStepBlocks
       nbx -= px.bw;
       ++nby;
     }
-    const uint64_t nq = load_row(nbx, nby, sb + 8u, k, r, rW, s + 1 < nsteps);
-    const bool on = sb + k < nb32;
-    const uint64_t v = row_symbols(q, r, px.delta, px.init_byte, &first_unused);
-    // codes MSB-first: pairs in 32 bits (v_lshl_or), then two chunks of four in 64
-    uint32_t pc[4], pl[4];
+    uint64_t na, nbq;
+    load_pair(nbx, nby, sb + kStepBlocks, s + 1 < nsteps, na, nbq);
+    const uint32_t ba = sb + 2u * k;
+    const bool on_a = ba < nb32, on_b = ba + 1u < nb32;
+    // codes MSB-first: pairs of symbols in 32 bits (v_lshl_or), chunks of four in 64
+    uint64_t ch[4];
+    uint32_t cl[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t e0 = tab[(uint32_t)(v >> (16 * j)) & 0xFFu], e1 = tab[(uint32_t)(v >> (16 * j + 8)) & 0xFFu];
-      const uint32_t l1 = e1 >> 16;
-      pc[j] = ((e0 & 0xFFFFu) << l1) | (e1 & 0xFFFFu);
-      pl[j] = (e0 >> 16) + l1;
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t v = row_symbols(h ? qb : qa, r, px.delta, px.init_byte, &first_unused);
+      uint32_t pc[4], pl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e0 = tab[(uint32_t)(v >> (16 * j)) & 0xFFu], e1 = tab[(uint32_t)(v >> (16 * j + 8)) & 0xFFu];
+        const uint32_t l1 = e1 >> 16;
+        pc[j] = ((e0 & 0xFFFFu) << l1) | (e1 & 0xFFFFu);
+        pl[j] = (e0 >> 16) + l1;
+      }
+      ch[2 * h] = ((uint64_t)pc[0] << pl[1]) | pc[1];
+      ch[2 * h + 1] = ((uint64_t)pc[2] << pl[3]) | pc[3];
+      cl[2 * h] = pl[0] + pl[1];
+      cl[2 * h + 1] = pl[2] + pl[3];
     }
-    const uint64_t ch[2] = {((uint64_t)pc[0] << pl[1]) | pc[1], ((uint64_t)pc[2] << pl[3]) | pc[3]};
-    const uint32_t cl[2] = {pl[0] + pl[1], pl[2] + pl[3]};
-    const uint32_t nbits = on ? cl[0] + cl[1] : 0u;
-    const uint32_t incl = wave_scan_dpp(nbits);
-    const uint32_t T = __builtin_amdgcn_readlane(incl, 63), pre = incl - nbits;
-    __builtin_amdgcn_raw_buffer_store_b32(pos + pre, ro, (int)(on && r == 0 ? (sb + k) * 4u : kOob), 0, 0);
+    const uint32_t na_bits = on_a ? cl[0] + cl[1] : 0u, nb_bits = on_b ? cl[2] + cl[3] : 0u;
+    // bit order: block 2 k (rows 0-7), then block 2 k + 1: one scan of A | B << 16 (each
+    // half's sum over the wave <= 8,192), the pair's start and its A total by broadcast
+    const uint32_t x = na_bits | (nb_bits << 16);
+    const uint32_t S = wave_scan_dpp(x), ex = S - x;
+    const uint32_t g = __shfl(ex, lane & ~7u), ge = __shfl(S, lane | 7u);
+    const uint32_t Tw = __builtin_amdgcn_readlane(S, 63);
+    const uint32_t T = (Tw & 0xFFFFu) + (Tw >> 16);
+    const uint32_t start = (g & 0xFFFFu) + (g >> 16);             // the pair's first bit (step-relative)
+    const uint32_t atot = (ge & 0xFFFFu) - (g & 0xFFFFu);         // block 2 k's bits
+    const uint32_t pa = (g >> 16) + (ex & 0xFFFFu);                // this row of block 2 k
+    const uint32_t pb = (g & 0xFFFFu) + atot + (ex >> 16);         // this row of block 2 k + 1
+    // block offsets: lane r = 0 writes block 2 k's, lane r = 1 block 2 k + 1's
+    const bool wo = r == 0 ? on_a : r == 1 ? on_b : false;
+    __builtin_amdgcn_raw_buffer_store_b32(pos + start + (r == 1 ? atot : 0u), ro, (int)(wo ? (ba + r) * 4u : kOob), 0,
+                                          0);
     const uint32_t rr = pos & 31u;
-    if (on) {
-      or_bits(lw, rr + pre, ch[0], cl[0]);
-      or_bits(lw, rr + pre + cl[0], ch[1], cl[1]);
+    if (on_a) {
+      or_bits(lw, rr + pa, ch[0], cl[0]);
+      or_bits(lw, rr + pa + cl[0], ch[1], cl[1]);
+    }
+    if (on_b) {
+      or_bits(lw, rr + pb, ch[2], cl[2]);
+      or_bits(lw, rr + pb + cl[2], ch[3], cl[3]);
     }
     wave_sync();
     // whole words out; the last partial word stays as the next step's first
     const uint32_t nfull = (rr + T) >> 5, w0 = pos >> 5, nq4 = nfull >> 2;
-    const v4u32 quad = lq[lane];                                   // words 4 lane .. 4 lane + 3
+    const v4u32 q0 = lq[lane], q1 = lq[64 + lane];                    // words 4 lane .., 256 + 4 lane ..
     const uint32_t tail = lw[min(4u * nq4 + lane, kStepSlots - 1u)];  // lanes < nfull % 4: the last words
     const uint32_t carry = lw[nfull];
-    __builtin_amdgcn_raw_buffer_store_b128(quad, rw, (int)(lane < nq4 ? (w0 + 4u * lane) * 4u : kOob), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(q0, rw, (int)(lane < nq4 ? (w0 + 4u * lane) * 4u : kOob), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(q1, rw, (int)(64u + lane < nq4 ? (w0 + 256u + 4u * lane) * 4u : kOob), 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(tail, rw, (int)(lane < (nfull & 3u) ? (w0 + 4u * nq4 + lane) * 4u : kOob), 0,
                                           0);
     wave_sync();
     clear_words(carry);
     wave_sync();
     pos += T;
-    q = nq;
+    qa = na;
+    qb = nbq;
     sbx = nbx;
     sby = nby;
-    sb += 8;
+    sb += kStepBlocks;
   }
   // the last tile writes its partial last word, then the zero pad up to the byte count
   // rounded to words (the others leave that word to the next tile)
@@ -1703,7 +1763,8 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
                        d_frame_code_offsets, f0, n_frames);
     Pixels px = px0;
     px.gray = gray;
-    hipLaunchKernelGGL(vec ? enc_pack_wave_kernel<true> : enc_pack_wave_kernel<false>,
+    hipLaunchKernelGGL((!vec ? enc_pack_wave_kernel<false, false>
+                            : bw % 2 ? enc_pack_wave_kernel<true, false> : enc_pack_wave_kernel<true, true>),
                        dim3((nt + kPackWaves - 1) / kPackWaves), dim3(kPackWaves * 64), 0, st, px, gray_frame_stride, nb,
                        (uint32_t)ncode, table, meta, to, d_block_offsets + (uint64_t)f0 * nb,
                        d_codes + f0 * codes_frame_stride, codes_frame_stride, nt);
