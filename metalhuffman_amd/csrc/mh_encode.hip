@@ -45,9 +45,6 @@ constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;  // a packer's wait limit: 1
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 constexpr uint32_t kFusedMaxTiles = 512;  // frames up to this many tiles take the two-kernel path
 
-#ifndef MH_SPLIT_RUNS  // A/B: merge runs of one symbol in a block row before the histogram atomics
-#define MH_SPLIT_RUNS 0
-#endif
 #ifndef MH_CODE_STAMPS  // diagnostic builds only: s_memrealtime phase stamps of enc_code_kernel
 #define MH_CODE_STAMPS 0
 #endif
@@ -313,23 +310,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
       if constexpr (!kTiled) {  // the four-kernel path's symbol buffer (large frames: 64-bit offsets)
         if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
       }
-#if MH_SPLIT_RUNS
-      // runs of one symbol in the row merged first: one atomic per run, not per symbol
-      uint32_t cur = (uint32_t)v & 0xFFu, n = 1;
-#pragma unroll
-      for (int j = 1; j < 8; ++j) {
-        const uint32_t sj = (uint32_t)(v >> (8 * j)) & 0xFFu;
-        if (sj != cur) {
-          atomicAdd(&h[cur * kHistCopies + copy], n);
-          cur = sj;
-          n = 0;
-        }
-        ++n;
-      }
-      atomicAdd(&h[cur * kHistCopies + copy], n);
-#else
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
-#endif
     }
   };
   // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
@@ -376,6 +357,64 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
 #endif
 }
 
+
+// The batched split, persistent: workgroup g counts tiles g, g + G, ... of all frames
+// (tile i = tile i % ncode of frame i / ncode) with the next tile's rows in flight while
+// one is counted, and reads and clears its histogram in one pass per tile. (One
+// workgroup per tile left each workgroup's HBM round trip, histogram clear and launch
+// ramp in series: 12 short-lived workgroup generations per CU.)
+template <bool kVec>
+__global__ void __launch_bounds__(256) enc_split_batch_kernel(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw,
+                                                              uint64_t nb, uint32_t flags, uint8_t *block_init,
+                                                              uint16_t *tile_hist, uint32_t ncode, uint64_t gray_stride,
+                                                              uint32_t total) {
+  __shared__ uint32_t h[256 * kHistCopies];
+  const uint32_t tid = threadIdx.x, r = tid & 7u, copy = tid % kHistCopies;
+  const bool delta = !(flags & MH_FLAG_NO_DELTA), init = block_init != nullptr;
+  uint32_t i = blockIdx.x;
+  if (i >= total) return;  // workgroup-uniform
+  // tile ti's rows (a dead, all out-of-range set when !live: a fixed count of loads)
+  const auto load = [&](uint32_t ti, bool live, uint64_t (&q)[kTileGroups]) {
+    const uint32_t f = ti / ncode, t = ti - f * ncode;
+    tile_rows<kVec>(gray + f * gray_stride, W, H, bw, live ? nb : 0ull, t * kCodeTile, r, q);
+  };
+  uint64_t q[kTileGroups];
+  load(i, true, q);
+  for (uint32_t j = tid; j < 256 * kHistCopies; j += 256) h[j] = 0;
+  lds_barrier();
+  const uint32_t nb32 = (uint32_t)nb;
+  while (true) {
+    const uint32_t inext = i + gridDim.x;
+    const bool more = inext < total;
+    uint64_t nq[kTileGroups];
+    load(more ? inext : i, more, nq);
+    const uint32_t f = i / ncode, t = i - f * ncode;
+    const __amdgpu_buffer_rsrc_t rinit = enc_rsrc(init ? block_init + (uint64_t)f * nb : nullptr, init ? nb : 0ull);
+#pragma unroll
+    for (uint32_t u = 0; u < kTileGroups; ++u) {
+      const uint32_t b = t * kCodeTile + u * 32u + (tid >> 3);
+      const bool on = b < nb32;
+      uint32_t first;
+      const uint64_t v = row_symbols(q[u], r, delta, init, &first);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && on ? b : kOob), 0, 0);
+      if (on)
+        for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+    }
+    lds_barrier();
+    // read and clear (rotated: the 16 copies of one bin sit in 16 banks)
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < kHistCopies; ++k) {
+      uint32_t *p = &h[tid * kHistCopies + ((k + tid) % kHistCopies)];
+      c += *p;
+      *p = 0;
+    }
+    tile_hist[(uint64_t)i * 256 + tid] = (uint16_t)c;  // <= kCodeTile * 64
+    lds_barrier();  // cleared before the next tile's atomics
+    if (!more) break;
+    i = inext;
+    for (uint32_t u = 0; u < kTileGroups; ++u) q[u] = nq[u];  // (fully unrolled by the compiler)
+  }
+}
 
 // Value of lane (lane ^ D) (64-lane wave): permlane32_swap for 32, ds_swizzle's xor
 // mode for 16 and 4, DPP (row rotate by 8, quad permutes) for 8, 2, 1.
@@ -1339,30 +1378,25 @@ __device__ __forceinline__ void wave_sync() {
 template <bool kVec, bool kPair>
 __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
-    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t total) {
-  __shared__ uint32_t s_tab[kPackWaves][256];
+    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t ncode_wg) {
+  // ncode_wg: workgroups per frame (ncode rounded up to kPackWaves tiles): a workgroup's
+  // waves pack tiles of ONE frame and share its table, at a fixed LDS address (the
+  // gathers need no per-wave base: one VALU per symbol for the address)
+  __shared__ uint32_t tab[256];
   __shared__ __attribute__((aligned(16))) uint32_t s_w[kPackWaves][kStepSlots];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, k = lane >> 3, r = lane & 7u;
-  const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * kPackWaves + wave);
-  if (i >= total) return;  // wave-uniform; no workgroup barrier follows
-  const uint32_t f = i / ncode, t = i - f * ncode;
-  if (!(uint32_t)meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (the tree's status): nothing written
-  uint32_t *tab = s_tab[wave];
-  uint32_t *lw = s_w[wave];
+  const uint32_t f = blockIdx.x / ncode_wg, t = (blockIdx.x - f * ncode_wg) * kPackWaves + wave;
+  if (!(uint32_t)meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (workgroup-uniform): nothing written
   {
     // the frame's table as len << 16 | right-aligned code (the tree's words hold the
     // code left-aligned in 16 bits): two symbols' codes combine in one v_lshl_or
-    uint4 v = reinterpret_cast<const uint4 *>(table + (uint64_t)f * 256)[lane];
-    const auto ra = [](uint32_t e) {
-      const uint32_t L = e & 0x1Fu;
-      return L ? (L << 16) | ((e >> 16) >> (16u - L)) : 0u;
-    };
-    v.x = ra(v.x);
-    v.y = ra(v.y);
-    v.z = ra(v.z);
-    v.w = ra(v.w);
-    reinterpret_cast<uint4 *>(tab)[lane] = v;
+    const uint32_t e = table[(uint64_t)f * 256 + threadIdx.x];
+    const uint32_t L = e & 0x1Fu;
+    tab[threadIdx.x] = L ? (L << 16) | ((e >> 16) >> (16u - L)) : 0u;
   }
+  lds_barrier();
+  if (t >= ncode) return;  // wave-uniform padding past the frame's last tile; no barrier follows
+  uint32_t *lw = s_w[wave];
   const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
   const uint8_t *gray = px.gray + f * gray_stride;
   const uint64_t b0 = (uint64_t)t * kCodeTile;
@@ -1745,6 +1779,12 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
   const Pixels px0{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
+  // the persistent split: eight 256-thread workgroups per CU (its LDS histogram admits ten)
+  int dev = -1, cus = 0;
+  if (!(s && hipStreamGetDevice(s, &dev) == hipSuccess) && hipGetDevice(&dev) != hipSuccess) return MH_ERR_HIP;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    return MH_ERR_HIP;
+  const uint32_t split_grid = 8u * (uint32_t)cus;
   // frames [f0, f0 + m): split, trees, packing on stream st
   const auto sub_batch = [&](hipStream_t st, uint32_t f0, uint32_t m) {
     const uint32_t nt = (uint32_t)(ncode * m);
@@ -1754,20 +1794,21 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
     uint32_t *table = w.table + (uint64_t)f0 * 256;
     uint64_t *meta = w.meta + (uint64_t)f0 * kMetaWords;
     uint32_t *to = w.tile_off + (uint64_t)f0 * (ncode + 1);
-    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, st,
-                       gray, width, height, bw, nb, flags, nullptr, binit, nullptr, th, nullptr, (uint32_t)ncode,
-                       gray_frame_stride);
+    hipLaunchKernelGGL((vec ? enc_split_batch_kernel<true> : enc_split_batch_kernel<false>),
+                       dim3(std::min<uint32_t>(nt, split_grid)), dim3(256), 0, st, gray, width, height, bw, nb, flags,
+                       binit, th, (uint32_t)ncode, gray_frame_stride, nt);
     hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(m), dim3(kTreeThreads), 0, st, nullptr,
                        d_canon_headers + (uint64_t)f0 * 256, table, meta, d_codes_len ? d_codes_len + f0 : nullptr,
                        codes_frame_stride, d_status ? d_status + f0 : nullptr, nb, th, (uint32_t)ncode, to,
                        d_frame_code_offsets, f0, n_frames);
     Pixels px = px0;
     px.gray = gray;
+    const uint32_t ncode_wg = (uint32_t)((ncode + kPackWaves - 1) / kPackWaves);
     hipLaunchKernelGGL((!vec ? enc_pack_wave_kernel<false, false>
                             : bw % 2 ? enc_pack_wave_kernel<true, false> : enc_pack_wave_kernel<true, true>),
-                       dim3((nt + kPackWaves - 1) / kPackWaves), dim3(kPackWaves * 64), 0, st, px, gray_frame_stride, nb,
-                       (uint32_t)ncode, table, meta, to, d_block_offsets + (uint64_t)f0 * nb,
-                       d_codes + f0 * codes_frame_stride, codes_frame_stride, nt);
+                       dim3(ncode_wg * m), dim3(kPackWaves * 64), 0, st, px, gray_frame_stride, nb, (uint32_t)ncode, table,
+                       meta, to, d_block_offsets + (uint64_t)f0 * nb, d_codes + f0 * codes_frame_stride,
+                       codes_frame_stride, ncode_wg);
   };
   // One sub-batch: splitting the call into sub-batches alternated over a second stream
   // (trees beside another sub-batch's split / packing) measured slower, and the packer's
