@@ -358,64 +358,6 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
 }
 
 
-// The batched split, persistent: workgroup g counts tiles g, g + G, ... of all frames
-// (tile i = tile i % ncode of frame i / ncode) with the next tile's rows in flight while
-// one is counted, and reads and clears its histogram in one pass per tile. (One
-// workgroup per tile left each workgroup's HBM round trip, histogram clear and launch
-// ramp in series: 12 short-lived workgroup generations per CU.)
-template <bool kVec>
-__global__ void __launch_bounds__(256) enc_split_batch_kernel(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw,
-                                                              uint64_t nb, uint32_t flags, uint8_t *block_init,
-                                                              uint16_t *tile_hist, uint32_t ncode, uint64_t gray_stride,
-                                                              uint32_t total) {
-  __shared__ uint32_t h[256 * kHistCopies];
-  const uint32_t tid = threadIdx.x, r = tid & 7u, copy = tid % kHistCopies;
-  const bool delta = !(flags & MH_FLAG_NO_DELTA), init = block_init != nullptr;
-  uint32_t i = blockIdx.x;
-  if (i >= total) return;  // workgroup-uniform
-  // tile ti's rows (a dead, all out-of-range set when !live: a fixed count of loads)
-  const auto load = [&](uint32_t ti, bool live, uint64_t (&q)[kTileGroups]) {
-    const uint32_t f = ti / ncode, t = ti - f * ncode;
-    tile_rows<kVec>(gray + f * gray_stride, W, H, bw, live ? nb : 0ull, t * kCodeTile, r, q);
-  };
-  uint64_t q[kTileGroups];
-  load(i, true, q);
-  for (uint32_t j = tid; j < 256 * kHistCopies; j += 256) h[j] = 0;
-  lds_barrier();
-  const uint32_t nb32 = (uint32_t)nb;
-  while (true) {
-    const uint32_t inext = i + gridDim.x;
-    const bool more = inext < total;
-    uint64_t nq[kTileGroups];
-    load(more ? inext : i, more, nq);
-    const uint32_t f = i / ncode, t = i - f * ncode;
-    const __amdgpu_buffer_rsrc_t rinit = enc_rsrc(init ? block_init + (uint64_t)f * nb : nullptr, init ? nb : 0ull);
-#pragma unroll
-    for (uint32_t u = 0; u < kTileGroups; ++u) {
-      const uint32_t b = t * kCodeTile + u * 32u + (tid >> 3);
-      const bool on = b < nb32;
-      uint32_t first;
-      const uint64_t v = row_symbols(q[u], r, delta, init, &first);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && on ? b : kOob), 0, 0);
-      if (on)
-        for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
-    }
-    lds_barrier();
-    // read and clear (rotated: the 16 copies of one bin sit in 16 banks)
-    uint32_t c = 0;
-    for (uint32_t k = 0; k < kHistCopies; ++k) {
-      uint32_t *p = &h[tid * kHistCopies + ((k + tid) % kHistCopies)];
-      c += *p;
-      *p = 0;
-    }
-    tile_hist[(uint64_t)i * 256 + tid] = (uint16_t)c;  // <= kCodeTile * 64
-    lds_barrier();  // cleared before the next tile's atomics
-    if (!more) break;
-    i = inext;
-    for (uint32_t u = 0; u < kTileGroups; ++u) q[u] = nq[u];  // (fully unrolled by the compiler)
-  }
-}
-
 // Value of lane (lane ^ D) (64-lane wave): permlane32_swap for 32, ds_swizzle's xor
 // mode for 16 and 4, DPP (row rotate by 8, quad permutes) for 8, 2, 1.
 template <uint32_t D>
@@ -1279,21 +1221,27 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
     if (f0 + f + 1 == n_frames) frame_off[n_frames] = (uint64_t)n_frames * codes_cap;
   }
   // the frame's symbol counts: the sum of its tile counts (wave w: tiles w, w + 16, ...,
-  // eight 8-byte loads in flight per lane, lane l: symbols 4l..4l+3), no global atomics
+  // 24 8-byte loads in flight per lane, lane l: symbols 4l..4l+3), no global atomics
   __shared__ uint32_t s_part[kCodeWaves][256], s_cnt[256];
   {
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     const uint2 *th = reinterpret_cast<const uint2 *>(tile_hist + (uint64_t)f * ncode * 256);
     uint32_t acc[4] = {0, 0, 0, 0};
-    for (uint32_t t0 = wave; t0 < ncode; t0 += kCodeWaves * 8u) {
-      uint2 v[8];
+    // 24 tiles per wave in flight (a 2048x1536 frame's 384 tiles in one round trip),
+    // unconditional buffer loads (tiles past the frame read zero)
+    constexpr uint32_t kDepth = 24;
+    const __amdgpu_buffer_rsrc_t rth = enc_rsrc(th, (uint64_t)ncode * 512u);
+    for (uint32_t t0 = wave; t0 < ncode; t0 += kCodeWaves * kDepth) {
+      uint2 v[kDepth];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
+      for (uint32_t k = 0; k < kDepth; ++k) {
         const uint32_t t = t0 + kCodeWaves * k;
-        v[k] = t < ncode ? th[(uint64_t)t * 64 + lane] : make_uint2(0u, 0u);
+        typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+        const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(rth, (int)(t < ncode ? t * 512u + lane * 8u : kOob), 0, 0);
+        v[k] = make_uint2(x.x, x.y);
       }
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
+      for (uint32_t k = 0; k < kDepth; ++k) {
         acc[0] += v[k].x & 0xFFFFu;
         acc[1] += v[k].x >> 16;
         acc[2] += v[k].y & 0xFFFFu;
@@ -1323,7 +1271,7 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
   // of 4 * kTileBatch tiles (lane l: symbols 4l..4l+3 of a tile, one 8-byte load; all
   // kTileBatch loads in flight); wave 0 scans the chunk's totals with a running carry.
   const uint32_t lane = tid & 63u, wave = tid >> 6;
-  const uint2 *th = reinterpret_cast<const uint2 *>(tile_hist + (uint64_t)f * ncode * 256);
+  const __amdgpu_buffer_rsrc_t rth = enc_rsrc(tile_hist + (uint64_t)f * ncode * 256, (uint64_t)ncode * 512u);
   uint32_t *to = tile_off + (uint64_t)f * (ncode + 1);
   const uint32_t l0 = s_len[4 * lane], l1 = s_len[4 * lane + 1], l2 = s_len[4 * lane + 2], l3 = s_len[4 * lane + 3];
   uint32_t carry = 0;
@@ -1331,11 +1279,17 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
     const uint32_t t0 = c + wave * kTileBatch;
     uint2 v[kTileBatch];
 #pragma unroll
-    for (uint32_t k = 0; k < kTileBatch; ++k)
-      v[k] = t0 + k < ncode ? th[(uint64_t)(t0 + k) * 64 + lane] : make_uint2(0u, 0u);
+    for (uint32_t k = 0; k < kTileBatch; ++k) {  // unconditional buffer loads (past the frame: zero)
+      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+      const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(rth, (int)(t0 + k < ncode ? (t0 + k) * 512u + lane * 8u : kOob),
+                                                           0, 0);
+      v[k] = make_uint2(x.x, x.y);
+    }
 #pragma unroll
     for (uint32_t k = 0; k < kTileBatch; ++k) {
-      uint32_t x = (v[k].x & 0xFFFFu) * l0 + (v[k].x >> 16) * l1 + (v[k].y & 0xFFFFu) * l2 + (v[k].y >> 16) * l3;
+      // counts < 2^15, lengths < 2^5: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate)
+      uint32_t x = __umul24(v[k].x & 0xFFFFu, l0) + __umul24(v[k].x >> 16, l1) + __umul24(v[k].y & 0xFFFFu, l2) +
+                   __umul24(v[k].y >> 16, l3);
       x = wave_scan_dpp(x);
       if (lane == 63) s_chunk[wave * kTileBatch + k] = x;  // the tile's bits (< 2^21)
     }
@@ -1779,12 +1733,6 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   flags &= ~MH_ENCODE_WORKSPACE_ZEROED;
   const uint32_t vec = (width % 8 == 0 && ((uintptr_t)d_gray & 7u) == 0 && (gray_frame_stride & 7u) == 0) ? 1u : 0u;
   const Pixels px0{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
-  // the persistent split: eight 256-thread workgroups per CU (its LDS histogram admits ten)
-  int dev = -1, cus = 0;
-  if (!(s && hipStreamGetDevice(s, &dev) == hipSuccess) && hipGetDevice(&dev) != hipSuccess) return MH_ERR_HIP;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-    return MH_ERR_HIP;
-  const uint32_t split_grid = 8u * (uint32_t)cus;
   // frames [f0, f0 + m): split, trees, packing on stream st
   const auto sub_batch = [&](hipStream_t st, uint32_t f0, uint32_t m) {
     const uint32_t nt = (uint32_t)(ncode * m);
@@ -1794,9 +1742,11 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
     uint32_t *table = w.table + (uint64_t)f0 * 256;
     uint64_t *meta = w.meta + (uint64_t)f0 * kMetaWords;
     uint32_t *to = w.tile_off + (uint64_t)f0 * (ncode + 1);
-    hipLaunchKernelGGL((vec ? enc_split_batch_kernel<true> : enc_split_batch_kernel<false>),
-                       dim3(std::min<uint32_t>(nt, split_grid)), dim3(256), 0, st, gray, width, height, bw, nb, flags,
-                       binit, th, (uint32_t)ncode, gray_frame_stride, nt);
+    // one workgroup per tile (a persistent split with the next tile's rows in flight
+    // measured slower: profiles/r04_v4_encoder_batch_ab.txt)
+    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, st,
+                       gray, width, height, bw, nb, flags, nullptr, binit, nullptr, th, nullptr, (uint32_t)ncode,
+                       gray_frame_stride);
     hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(m), dim3(kTreeThreads), 0, st, nullptr,
                        d_canon_headers + (uint64_t)f0 * 256, table, meta, d_codes_len ? d_codes_len + f0 : nullptr,
                        codes_frame_stride, d_status ? d_status + f0 : nullptr, nb, th, (uint32_t)ncode, to,

@@ -93,10 +93,14 @@ def test_batch_mixed_histograms_and_rejected_frame(mh, device, bigbridge):
     _check_batch(mh, device, imgs, expect_bad=(3,))
 
 
-@pytest.mark.parametrize("hw", [(1, 1), (9, 17), (1001, 777), (8, 4096), (2056, 2048)])
+@pytest.mark.parametrize("hw", [(1, 1), (9, 17), (1001, 777), (8, 4096), (2056, 2048),
+                                (64, 776), (72, 24), (80, 48), (136, 1032)])
 def test_batch_odd_sizes_and_variants(mh, device, bigbridge, hw):
     """Partial edge blocks, one-block frames, tile counts that are not a multiple of
-    the tile-offset chunk, frames larger than the single-frame fused path; the
+    the tile-offset chunk or of the packer's four waves per workgroup, frames larger than
+    the single-frame fused path; every packer row loader: byte loads (W % 8 != 0), one
+    8-byte load per block (W % 8 == 0 with an odd width in blocks: 776, 24, 1032), one
+    16-byte load per block pair (an even width in blocks, narrower than a step: 48); the
     init-byte and no-delta formats."""
     from metalhuffman_amd import frames as F
     h, w = hw
