@@ -113,7 +113,7 @@ uint64_t carve(uint8_t *base, uint64_t nb, Workspace *w) {
 // row up, histogram into 16 replicated LDS copies (BigBridge-like deltas are mostly
 // one symbol; one copy would serialise every atomic on it). Grid-stride over groups
 // of 32 blocks; one global atomic per used bin per workgroup.
-constexpr uint32_t kHistCopies = 16;
+constexpr uint32_t kHistCopies = 16;  // 8: no faster, 32: 58 % slower (profiles/r04_v4_encoder_batch_ab.txt)
 constexpr uint32_t kSplitBatch = 8;   // groups of 32 blocks whose rows a split workgroup loads at once
 constexpr uint32_t kSplitWgs = 256;   // split workgroups (four-kernel path): one global atomic per used bin each
 
