@@ -284,12 +284,14 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     meta[kGen] += 1;  // a new tag for the code table words (table_tag)
   }
   MH_SPLIT_STAMP(0)
-  __shared__ uint32_t h[256 * kHistCopies];
+  __shared__ __attribute__((aligned(16))) uint32_t h[256 * kHistCopies];
   // the histogram is cleared behind the first batch's loads (their HBM round trip
-  // covers it), before any atomic
+  // covers it), before any atomic: 16-byte writes, consecutive per lane (no conflicts)
   bool cleared = false;
   const auto clear_hist = [&]() {
-    for (uint32_t i = threadIdx.x; i < 256 * kHistCopies; i += 256) h[i] = 0;
+    typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (uint32_t i = 0; i < kHistCopies / 4; ++i) reinterpret_cast<v4u32 *>(h)[threadIdx.x + 256u * i] = v4u32{0u, 0u, 0u, 0u};
     lds_barrier();
     cleared = true;
   };
@@ -302,7 +304,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   // fused path's packer re-derives them from the pixels), histogram
   auto process = [&](uint64_t g, uint64_t q) {
     const uint64_t b = g * 32 + (threadIdx.x >> 3);
-    const bool on = b < nb;
+    const bool on = kTiled ? (uint32_t)b < (uint32_t)nb : b < nb;  // tiled: one frame, < 2^26 blocks
     uint32_t first;
     const uint64_t v = row_symbols(q, r, delta, block_init != nullptr, &first);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && on ? (uint32_t)b : kOob), 0, 0);

@@ -5,7 +5,9 @@ replays exactly. Every case: the product's host codec encodes a generated frame
 (byte-identical to the reference encoder, test_codec_parity.py); the GPU decodes it
 through the C-ABI and must return the input. Every 8th case (up to 1 Mpixel) is also
 compared with the oracle's shader-semantics decode, every 4th case's GPU encoder
-output (header, code bytes, block offsets, init bytes) with the host codec's.
+output (header, code bytes, block offsets, init bytes) with the host codec's, and
+every batch of frames sharing a table is also GPU-encoded in one batched call
+(mh_encode_frames_device_async) and compared frame by frame.
 
 Frame kinds: natural-like (geometric steps), Gaussian noise, uniform bytes, sparse
 alphabets (2-6 symbols), a constant frame (one-symbol alphabet), Fibonacci histograms
@@ -73,12 +75,12 @@ def test_randomized_parity_sweep(mh, oracle, device, bigbridge):
     from metalhuffman_amd import _native as N
     from metalhuffman_amd import decoder as D
     from metalhuffman_amd import frames as F
-    from metalhuffman_amd.encoder import encode_frame_device
+    from metalhuffman_amd.encoder import BatchEncoder, encode_frame_device
 
     budget = float(os.environ.get("MH_STRESS_SECONDS", "15"))
     first = int(os.environ.get("MH_STRESS_FIRST_CASE", "0"))
     t_end = time.perf_counter() + budget
-    stats = {"cases": 0, "rejected": 0, "oracle": 0, "encoder": 0, "pixels": 0}
+    stats = {"cases": 0, "rejected": 0, "oracle": 0, "encoder": 0, "batch_encoder": 0, "pixels": 0}
     per_mode = dict.fromkeys(MODES, 0)
     case = first
     last_report = time.perf_counter()
@@ -107,6 +109,19 @@ def test_randomized_parity_sweep(mh, oracle, device, bigbridge):
             torch.cuda.synchronize(device)
             bad = [i for i in range(n) if not torch.equal(out[i, :, :w], refs[i])]
             assert not bad, (tag, bad)
+            # the batched GPU encoder on the same frames: byte-identical frame by frame
+            benc = BatchEncoder(w, h, n, device)
+            a = benc.encode_async(refs, ef.flags & 1, fmt == 2)
+            torch.cuda.synchronize(device)
+            for i, e in enumerate(efs):
+                r = a.frame(i)
+                assert int(a.status[i].item()) == 0, (tag, i)
+                assert np.array_equal(r.canon, e.canon), (tag, i)
+                assert np.array_equal(r.codes.cpu().numpy(), e.codes), (tag, i)
+                assert np.array_equal(r.block_offsets.cpu().numpy().view(np.uint32), e.block_offsets), (tag, i)
+                if fmt == 2:
+                    assert np.array_equal(r.block_init.cpu().numpy(), e.block_init), (tag, i)
+            stats["batch_encoder"] += n
         elif mode == "any_order":
             frs = D.DeviceFrames.pack([ef], device)
             outs = [D.decode(frs, tabs, extra_flags=N.MH_FLAG_ANY_ORDER if k else 0) for k in range(3)]
