@@ -794,7 +794,9 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 #pragma unroll
     for (int k = 0; k < kLutLoads; ++k) dst[threadIdx.x + 64u * kSmallWaves * k] = L[k];
   }
-  __syncthreads();  // table in LDS
+  // table in LDS: an LDS-only barrier (waits lgkmcnt, not vmcnt), so no wave waits here
+  // for another wave's span (HBM, cold); each waits for its own span at its first read
+  lds_barrier();
   MH_STAMP(2);
   if (!live) return;  // no barrier below
   const OutTile ot = out_tile(a, t, lane);
