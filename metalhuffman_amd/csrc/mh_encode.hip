@@ -1209,7 +1209,7 @@ __global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_code_kernel(u
 // workgroup's ~10 us tree each (the single-frame path): the N trees run side by side.
 constexpr uint32_t kMetaWords = 32;  // per-frame meta slots (>= kGen + 1)
 static_assert(kMetaWords >= kGen + 1, "meta slots");
-constexpr uint32_t kTileBatch = 32;  // tiles per wave and chunk of the tile-offset pass
+constexpr uint32_t kTileBatch = 16;  // tiles per wave and chunk of the tile-offset pass
 
 __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
     uint64_t *hist, uint8_t *canon, uint32_t *table, uint64_t *meta, uint64_t *codes_len, uint64_t codes_cap,
@@ -1266,27 +1266,33 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
                                       codes_cap, status ? status + f : nullptr, nb * 64, s_cnt);
   if (tid >= 256) return;  // tree_body leaves the 256 symbol threads (4 waves)
   __shared__ uint32_t s_len[256], s_chunk[4 * kTileBatch];
+  static_assert(4 * kTileBatch == 64, "one chunk total per lane of wave 0");
   s_len[tid] = e & 0x1Fu;
   lds_barrier();
   if (e & 0x80u) return;  // rejected frame (uniform): the pack kernel writes nothing
   // Tile offsets: wave w reduces tiles c + w * kTileBatch + [0, kTileBatch) of each chunk
-  // of 4 * kTileBatch tiles (lane l: symbols 4l..4l+3 of a tile, one 8-byte load; all
-  // kTileBatch loads in flight); wave 0 scans the chunk's totals with a running carry.
+  // of 4 * kTileBatch = 64 tiles (lane l: symbols 4l..4l+3 of a tile, one 8-byte load),
+  // the next chunk's loads in flight while one is reduced; wave 0 scans the chunk's
+  // totals (one per lane) with a running carry. Loads and stores are unconditional
+  // buffer operations (out of range past the frame), so vmcnt counts them exactly.
   const uint32_t lane = tid & 63u, wave = tid >> 6;
   const __amdgpu_buffer_rsrc_t rth = enc_rsrc(tile_hist + (uint64_t)f * ncode * 256, (uint64_t)ncode * 512u);
   uint32_t *to = tile_off + (uint64_t)f * (ncode + 1);
+  const __amdgpu_buffer_rsrc_t rto = enc_rsrc(to, (uint64_t)(ncode + 1) * 4u);
   const uint32_t l0 = s_len[4 * lane], l1 = s_len[4 * lane + 1], l2 = s_len[4 * lane + 2], l3 = s_len[4 * lane + 3];
-  uint32_t carry = 0;
-  for (uint32_t c = 0; c < ncode; c += 4 * kTileBatch) {
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+  const auto load_chunk = [&](uint32_t c, v2u32 (&v)[kTileBatch]) {
     const uint32_t t0 = c + wave * kTileBatch;
-    uint2 v[kTileBatch];
 #pragma unroll
-    for (uint32_t k = 0; k < kTileBatch; ++k) {  // unconditional buffer loads (past the frame: zero)
-      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-      const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(rth, (int)(t0 + k < ncode ? (t0 + k) * 512u + lane * 8u : kOob),
-                                                           0, 0);
-      v[k] = make_uint2(x.x, x.y);
-    }
+    for (uint32_t k = 0; k < kTileBatch; ++k)
+      v[k] = __builtin_amdgcn_raw_buffer_load_b64(rth, (int)(t0 + k < ncode ? (t0 + k) * 512u + lane * 8u : kOob), 0, 0);
+  };
+  uint32_t carry = 0;
+  v2u32 v[kTileBatch];
+  load_chunk(0, v);
+  for (uint32_t c = 0; c < ncode; c += 4 * kTileBatch) {
+    v2u32 nv[kTileBatch];
+    load_chunk(c + 4 * kTileBatch, nv);  // past the frame: all out of range
 #pragma unroll
     for (uint32_t k = 0; k < kTileBatch; ++k) {
       // counts < 2^15, lengths < 2^5: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate)
@@ -1296,16 +1302,15 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
       if (lane == 63) s_chunk[wave * kTileBatch + k] = x;  // the tile's bits (< 2^21)
     }
     lds_barrier();
-    if (wave == 0) {
-      // 4 * kTileBatch = 128 totals: two per lane
-      const uint32_t a = s_chunk[2 * lane], b = s_chunk[2 * lane + 1];
-      const uint32_t incl = wave_scan_dpp(a + b);
-      const uint32_t base = carry + incl - (a + b);
-      if (c + 2 * lane < ncode) to[c + 2 * lane] = base;
-      if (c + 2 * lane + 1 < ncode) to[c + 2 * lane + 1] = base + a;
+    if (wave == 0) {  // 4 * kTileBatch = 64 totals: one per lane
+      const uint32_t a = s_chunk[lane];
+      const uint32_t incl = wave_scan_dpp(a);
+      __builtin_amdgcn_raw_buffer_store_b32(carry + incl - a, rto, (int)(c + lane < ncode ? (c + lane) * 4u : kOob), 0, 0);
       carry += __builtin_amdgcn_readlane(incl, 63);
     }
     lds_barrier();
+#pragma unroll
+    for (uint32_t k = 0; k < kTileBatch; ++k) v[k] = nv[k];
   }
   if (tid == 0) to[ncode] = carry;
 }
