@@ -1198,14 +1198,14 @@ __global__ void __launch_bounds__(kCodeThreads, kCodeMinWaves) enc_code_kernel(u
   pack_tile(blockIdx.x - 1, px, tile_hist, table, meta, nb, ntiles, offsets, words, codes_cap, status);
 }
 
-// ---- batched frames: enc_split_kernel (tiled) + enc_tree_batch_kernel + enc_pack_batch_kernel
+// ---- batched frames: enc_split_kernel (tiled) + enc_tree_batch_kernel + enc_pack_wave_kernel
 // N independent frames of one size, each with its own histogram, tree and code table,
 // in three launches whatever N (mh_encode_frames_device_async). The kernel boundaries
 // order the phases, so no workgroup waits on another: the split (N x tiles workgroups)
 // writes per-tile symbol counts; workgroup f of the tree kernel builds frame f's tree
 // (tree_body) and then the frame's tile offsets (each tile's bits = its counts x the
-// code lengths, exclusive scan); the pack kernel (N x tiles workgroups) turns each
-// tile into code words from its first bit. Frames no longer queue behind one
+// code lengths, exclusive scan); the pack kernel (one wave per tile, four tiles of one
+// frame per workgroup) turns each tile into code words from its first bit. Frames no longer queue behind one
 // workgroup's ~10 us tree each (the single-frame path): the N trees run side by side.
 constexpr uint32_t kMetaWords = 32;  // per-frame meta slots (>= kGen + 1)
 static_assert(kMetaWords >= kGen + 1, "meta slots");

@@ -1,7 +1,7 @@
 """Batched device encoder (mh_encode_frames_device_async) on n BigBridge block
 shuffles per call: wall and HIP-event time per frame, calls back to back on one
 stream; run under rocprofv3 --kernel-trace --stats for the per-kernel split
-(enc_split_kernel / enc_tree_batch_kernel / enc_pack_batch_kernel).
+(enc_split_kernel / enc_tree_batch_kernel / enc_pack_wave_kernel).
 
     python scripts/enc_batch_profile.py [n_frames] [calls]
 """
