@@ -1323,6 +1323,7 @@ __global__ void __launch_bounds__(kTreeThreads) enc_tree_batch_kernel(
 // barriers per tile, profiles/r04_v4_encoder_batch_ab.txt). The next step's rows are in
 // flight while a step is packed (a fixed count of unconditional buffer loads).
 constexpr uint32_t kPackWaves = 4;     // waves per workgroup (independent of each other)
+static_assert(kPackWaves * 64 >= 256, "one table word per thread");
 constexpr uint32_t kStepBlocks = 16;
 constexpr uint32_t kStepSlots = 528;   // LDS words per wave (132 quads): a step's <= 513 words + or_bits' reach
 static_assert(kStepSlots >= kStepBlocks * 64 * 16 / 32 + 4 && kStepSlots % 4 == 0 && kStepSlots / 4 - 128 <= 64,
