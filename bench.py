@@ -36,6 +36,7 @@ import argparse
 import concurrent.futures as cf
 import json
 import os
+import socket
 import sys
 import time
 
@@ -954,10 +955,24 @@ def main(argv=None) -> int:
     ref_shape = wl.refs[0].shape[1:]
     # multi-rank: every rank's verified-frame count gathered on rank 0
     ranks_ok = None
+    rank_devices = None
     if use_dist:
+        # self-proving multi-GPU run: each rank's HIP ordinal and
+        # PCI bus id travel with its verified-frame count; under RCCL the (host, bus id)
+        # pairs must be distinct, i.e. N ranks on N physical GPUs
+        pci = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(pci, ctypes.c_int(64), ctypes.c_int(local)) != 0:
+            raise SystemExit(f"rank {rank}: hipDeviceGetPCIBusId failed")
+        me = {"rank": rank, "ordinal": int(torch.cuda.current_device()), "pci": pci.value.decode(),
+              "host": socket.gethostname()}
         got = [None] * world
-        dist.all_gather_object(got, (frames_verified, sum(f.n_frames for f in wl.launches)))
-        ranks_ok = sum(1 for a, b in got if a == b)
+        dist.all_gather_object(got, (frames_verified, sum(f.n_frames for f in wl.launches), me))
+        devs = {(g[2]["host"], g[2]["pci"]) for g in got}
+        if backend == "nccl" and len(devs) != world:
+            raise SystemExit(f"ranks share a GPU: {[g[2] for g in got]}")
+        ranks_ok = sum(1 for a, b, _ in got if a == b) if len(devs) == world or backend != "nccl" else 0
+        rank_devices = {"devices": [{k: g[2][k] for k in ("rank", "ordinal", "pci")} for g in got],
+                        "distinct_devices": len(devs), "backend": backend}
 
     wall, region_ms, kms = wl.run(args.steps, args.warmup, use_graph=not args.no_graph, world=world)
     wl.check_outputs()  # the any-order / rotated regions' rasters
@@ -997,6 +1012,7 @@ def main(argv=None) -> int:
     result["source_stamp"] = dict(B.source_stamps(), loaded=mh.lib().mh_build_stamp().decode()[:16])
     if ranks_ok is not None:
         result["ranks_verified"] = ranks_ok
+        result["rank_devices"] = rank_devices
     if t_bcast_us is not None:
         result["table_broadcast_us"] = round(t_bcast_us, 1)  # 256-B RCCL broadcast + device table build
         result["table_broadcast_bytes"] = 256

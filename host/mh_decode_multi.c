@@ -27,7 +27,8 @@
  *       N devices (<= hipGetDeviceCount), F frames per device per launch; the base
  *       frame is the raw W x H file (e.g. BigBridge) or a synthetic 2048 x 1536 one.
  *
- * Prints one line "multi ok N ..." (exit 0), or the first failure (exit 1 / 2).
+ * Prints one line per device (its HIP ordinal and PCI bus id; the ids must be distinct),
+ * then one line "multi ok N ... devices_verified N" (exit 0), or the failures (exit 1 / 2).
  */
 #define _POSIX_C_SOURCE 200809L
 #include <hip/hip_runtime_api.h>
@@ -79,6 +80,7 @@ typedef struct {
   float us_per_launch;
   int ok;
   char msg[256];
+  char pci[64];               /* the device's PCI bus id (hipDeviceGetPCIBusId) */
 } Worker;
 
 static void *xmalloc(size_t n) {
@@ -135,6 +137,7 @@ static void *worker(void *arg) {
   const int F = k->n_frames;
   const size_t px = (size_t)w * h, pitch = w;
   HIP_OK(hipSetDevice(k->dev));
+  HIP_OK(hipDeviceGetPCIBusId(k->pci, (int)sizeof(k->pci), k->dev));
   hipStream_t st;
   HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
 
@@ -220,26 +223,33 @@ static void *worker(void *arg) {
   fr.dims.block_width = bw;
   fr.dims.block_height = bh;
   fr.n_frames = (uint32_t)F;
-  MH_OK_OR_DIE(mh_decode(&fr, d_out, pitch, px, st)); /* warm-up */
-  HIP_OK(hipStreamSynchronize(st));
+  /* A rejected shard (a frame's encode status, a header that differs from the
+   * broadcast one, the table build) is never decoded: its offsets / slots were not
+   * written or do not match the tables. Its thread still meets the others at both
+   * barriers, so no device blocks, and reports FAIL without timing numbers. */
+  if (k->ok) {
+    MH_OK_OR_DIE(mh_decode(&fr, d_out, pitch, px, st)); /* warm-up */
+    HIP_OK(hipStreamSynchronize(st));
+  }
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   pthread_barrier_wait(k->bar);
   if (k->dev == 0) k->walls[0] = now_s();
   HIP_OK(hipEventRecord(e0, st));
-  for (int r = 0; r < k->reps; ++r) MH_OK_OR_DIE(mh_decode(&fr, d_out, pitch, px, st));
+  if (k->ok)
+    for (int r = 0; r < k->reps; ++r) MH_OK_OR_DIE(mh_decode(&fr, d_out, pitch, px, st));
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipStreamSynchronize(st));
   pthread_barrier_wait(k->bar);
   if (k->dev == 0) k->walls[1] = now_s();
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-  k->us_per_launch = k->reps ? 1e3f * ms / (float)k->reps : 0.f;
+  k->us_per_launch = k->reps && k->ok ? 1e3f * ms / (float)k->reps : 0.f;
 
   /* every decoded raster against its input frame */
   uint8_t *got = (uint8_t *)xmalloc(px * F);
-  HIP_OK(hipMemcpy(got, d_out, px * F, hipMemcpyDeviceToHost));
+  if (k->ok) HIP_OK(hipMemcpy(got, d_out, px * F, hipMemcpyDeviceToHost));
   for (int f = 0; f < F && k->ok; ++f)
     if (memcmp(got + px * f, frames + px * f, px)) {
       snprintf(k->msg, sizeof(k->msg), "device %d frame %d: decoded raster differs from the input", k->dev, f);
@@ -305,6 +315,19 @@ int main(int argc, char **argv) {
   for (int d = 0; d < n; ++d) pthread_join(th[d], NULL);
   int ok = 1;
   float worst = 0.f;
+  /* self-proving multi-GPU run: each worker's HIP ordinal and PCI bus id; N distinct
+   * bus ids mean N physical GPUs took part (not one GPU visible N times) */
+  int distinct = 1;
+  for (int d = 0; d < n; ++d) {
+    printf("device %d ordinal %d pci %s us_per_launch %.2f %s\n", d, ws[d].dev, ws[d].pci, ws[d].us_per_launch,
+           ws[d].ok ? "ok" : "FAIL");
+    for (int e = 0; e < d; ++e)
+      if (!strcmp(ws[d].pci, ws[e].pci)) distinct = 0;
+  }
+  if (!distinct) {
+    printf("FAIL devices do not have distinct PCI bus ids\n");
+    ok = 0;
+  }
   for (int d = 0; d < n; ++d) {
     if (!ws[d].ok) {
       printf("FAIL %s\n", ws[d].msg);
@@ -318,8 +341,8 @@ int main(int argc, char **argv) {
   const double wall_us = (walls[1] - walls[0]) * 1e6 / (reps ? reps : 1);
   const double pixels = (double)w * h * F * n;
   printf("multi ok %d devices %d frames_per_device %u %u reps %d broadcast_bytes 256 worst_device_us_per_launch "
-         "%.2f wall_us_per_launch %.2f MBps_events %.1f MBps_wall %.1f\n",
-         n, F, w, h, reps, worst, wall_us, worst > 0 ? pixels / worst : 0.0, wall_us > 0 ? pixels / wall_us : 0.0);
+         "%.2f wall_us_per_launch %.2f MBps_events %.1f MBps_wall %.1f devices_verified %d\n",
+         n, F, w, h, reps, worst, wall_us, worst > 0 ? pixels / worst : 0.0, wall_us > 0 ? pixels / wall_us : 0.0, n);
   free(ws);
   free(base);
   return 0;

@@ -66,12 +66,15 @@ extern "C" {
 /* decode flags */
 #define MH_FLAG_NO_DELTA 0x1u    /* IMPL_DELTAS_BEFORE_HUFF_ENCODING off
                                     (AAPLShaders.metal:263-265): emit symbols raw */
-#define MH_FLAG_LANE_PAIRS 0x2u  /* experimental (A/B): small launches (one frame)
-                                    decode each block with a lane pair -- one lane
-                                    from the block start, one speculatively from
-                                    its middle bit, re-synchronised through
-                                    ds_bpermute; same output. Ignored by batch
-                                    launches */
+#define MH_FLAG_LANE_PAIRS 0x2u  /* diagnostic only: mh_decode returns
+                                    MH_ERR_INVALID_ARG for it. The lane-pair kernel
+                                    (each block on two lanes -- one from the block
+                                    start, one speculatively from its middle bit,
+                                    re-synchronised through ds_bpermute; same output;
+                                    3.5x slower) is in the
+                                    diagnostic library libmh_diag_lanepairs.so, whose
+                                    mh_diag_decode_lanepairs takes mh_decode's
+                                    arguments */
 #define MH_FLAG_ANY_ORDER 0x4u   /* the launch may start before earlier work on
                                     the stream has finished (the AQL dispatch packet
                                     goes out without its barrier bit, HIP's
@@ -131,8 +134,11 @@ typedef struct {
 /* GPU decode (the hot path).                                              */
 
 /* Decode n_frames frames into d_out: frame f, row y starts at
- * d_out + f*out_frame_stride + y*out_pitch; W bytes per row are written.
- * out_pitch must be a multiple of 8 (the kernel stores 8-pixel block rows).
+ * d_out + f*out_frame_stride + y*out_pitch. round_up(W, 8) bytes of each row
+ * y < H are written (the kernel stores whole 8-pixel block rows, so a right-edge
+ * block also writes the padding between W and round_up(W, 8)); the rest of the
+ * pitch and rows >= H are not touched. out_pitch must be a multiple of 8 and
+ * >= W (hence >= round_up(W, 8): rows never overlap).
  * Asynchronous on `stream`; one kernel launch. */
 int mh_decode(const mh_frame *frame, uint8_t *d_out, size_t out_pitch,
               size_t out_frame_stride, void *stream);

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("MH_LIB") or os.path.join(_PKG, "libmetalhuffman_amd.s
 
 MH_OK = 0
 MH_FLAG_NO_DELTA = 0x1
-MH_FLAG_LANE_PAIRS = 0x2  # experimental lane-pair single-frame decode (A/B)
+MH_FLAG_LANE_PAIRS = 0x2  # lane-pair single-frame decode: diagnostic library only (diag_lanepairs())
 MH_FLAG_ANY_ORDER = 0x4  # the launch may overlap earlier work on the stream (caller guarantees independence)
 MH_ENCODE_WORKSPACE_ZEROED = 0x100  # the encoder workspace was zero-filled once (mh_encode_frame_device*)
 MH_CODES_PAD = 4
@@ -75,6 +75,32 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u16p = ctypes.POINTER(ctypes.c_uint16)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+_diag_lp = None
+
+
+def diag_lanepairs() -> ctypes.CDLL:
+    """The lane-pair diagnostic library (metalhuffman_amd/diag/libmh_diag_lanepairs.so,
+    built by `python -m metalhuffman_amd.build`): north_star's lane-group cursor, a
+    measured negative kept for A/B and its parity tests. It exports
+    one entry point, mh_diag_decode_lanepairs, with mh_decode's signature; the product
+    library refuses MH_FLAG_LANE_PAIRS."""
+    global _diag_lp
+    if _diag_lp is None:
+        from . import build as _build
+        path = _build.diag_lib_path("lanepairs")
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not found: build it with `python -m metalhuffman_amd.build`")
+        L = ctypes.CDLL(path)
+        L.mh_build_stamp.restype = ctypes.c_char_p
+        want, have = "diag:lanepairs:" + _build.diag_stamp("lanepairs"), L.mh_build_stamp().decode()
+        if have != want:
+            raise ImportError(f"{path} was built from other sources: rebuild with `python -m metalhuffman_amd.build`")
+        L.mh_diag_decode_lanepairs.argtypes = [ctypes.POINTER(mh_frame), _vp, ctypes.c_size_t, ctypes.c_size_t,
+                                               _vp]
+        _diag_lp = L
+    return _diag_lp
 
 
 def lib() -> ctypes.CDLL:

@@ -94,6 +94,29 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def ensure_objects(force: bool = False, verbose: bool = False, only=None) -> list[str]:
+    """Compile every default object (or those in `only`) whose content stamp is missing
+    or stale, whatever the library's stamp says; returns the objects' paths. The
+    diagnostic libraries link these objects, and _build/ does not travel to the GPU box,
+    so they must not assume build() left them behind (it returns early on a current
+    library)."""
+    os.makedirs(BUILD, exist_ok=True)
+    objs = []
+    for obj, (src, cmd) in SOURCES.items():
+        obj_path = os.path.join(BUILD, obj)
+        objs.append(obj_path)
+        if only is not None and obj not in only:
+            continue
+        st = object_stamp(obj)
+        if force or not _stamp_ok(obj_path, st):
+            full = cmd + [os.path.join(CSRC, src), "-o", obj_path]
+            if verbose:
+                print(" ".join(full), flush=True)
+            subprocess.run(full, check=True)
+            _write_stamp(obj_path, st)
+    return objs
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Rebuild by CONTENT, not mtime (a snapshot may carry any mtimes), and link the
     library with its stamp compiled in, so the loader can refuse a stale one.
@@ -106,19 +129,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     lst = library_stamp()
     if not force and _stamp_ok(LIB, lst):
         return LIB
-    os.makedirs(BUILD, exist_ok=True)
-    objs = []
-    for obj, (src, cmd) in SOURCES.items():
-        src_path = os.path.join(CSRC, src)
-        obj_path = os.path.join(BUILD, obj)
-        objs.append(obj_path)
-        st = object_stamp(obj)
-        if force or not _stamp_ok(obj_path, st):
-            full = cmd + [src_path, "-o", obj_path]
-            if verbose:
-                print(" ".join(full), flush=True)
-            subprocess.run(full, check=True)
-            _write_stamp(obj_path, st)
+    objs = ensure_objects(force=force, verbose=verbose)
     if force or not _stamp_ok(LIB, lst):
         stamp_c = os.path.join(BUILD, "mh_stamp.c")
         with open(stamp_c, "w") as f:
@@ -137,10 +148,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 DIAG_DIR = os.path.join(PKG, "diag")
-# Diagnostic libraries the GPU tests load in a child process (MH_LIB): name -> (-D
-# flags, the objects they change; the rest are the default build's objects)
+# Diagnostic libraries: name -> (-D flags, the objects they change, standalone).
+#   not standalone: the default library with some objects rebuilt, loaded INSTEAD of it
+#     (MH_LIB) in a child process by the GPU tests;
+#   standalone: only the changed objects (+ a stamp), loaded BESIDE the product library
+#     (_native.diag_lanepairs()). The lane-pair kernel (MH_FLAG_LANE_PAIRS, a measured
+#     negative kept for A/B) lives only there: the product library does not carry it.
 DIAG_LIBS = {
-    "spin0": (["MH_DIAG_SPIN_TICKS=0"], ["mh_encode.o"]),  # encoder packers time out at once
+    "spin0": (["MH_DIAG_SPIN_TICKS=0"], ["mh_encode.o"], False),  # encoder packers time out at once
+    "lanepairs": (["MH_LANE_PAIRS=1"], ["mh_decode.o"], True),    # exports mh_diag_decode_lanepairs
 }
 
 
@@ -148,21 +164,31 @@ def diag_lib_path(name: str) -> str:
     return os.path.join(DIAG_DIR, f"libmh_diag_{name}.so")
 
 
+def diag_stamp(name: str) -> str:
+    """The stamp compiled into a diagnostic library (after "diag:<name>:")."""
+    defines = DIAG_LIBS[name][0]
+    return _sha("diag", name, *defines, library_stamp())
+
+
 def build_diag(force: bool = False, verbose: bool = False) -> list[str]:
     """The diagnostic libraries (content-stamped like the default one)."""
     build(verbose=verbose)
     os.makedirs(DIAG_DIR, exist_ok=True)
     out = []
-    for name, (defines, changed) in DIAG_LIBS.items():
+    for name, (defines, changed, standalone) in DIAG_LIBS.items():
         lib = diag_lib_path(name)
-        stamp = _sha("diag", name, *defines, library_stamp())
+        stamp = diag_stamp(name)
         out.append(lib)
         if not force and _stamp_ok(lib, stamp):
             continue
         tmpdir = os.path.join(BUILD, f"diag_{name}")
         os.makedirs(tmpdir, exist_ok=True)
+        if not standalone:
+            ensure_objects(verbose=verbose, only=[o for o in SOURCES if o not in changed])
         objs = []
         for obj, (src, cmd) in SOURCES.items():
+            if standalone and obj not in changed:
+                continue
             if obj in changed:
                 o = os.path.join(tmpdir, obj)
                 full = cmd + [f"-D{d}" for d in defines] + [os.path.join(CSRC, src), "-o", o]

@@ -17,8 +17,11 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
+
+#include <pthread.h>
 
 #include "../../include/metalhuffman.h"
 
@@ -142,13 +145,25 @@ inline void decode_group(const uint16_t *flat, const uint8_t *codes, const uint3
 
 // Persistent worker pool for mh_decode_frame_cpu. Round 3 started fresh threads on
 // every call: 16 threads reached 5.6 x10^3 MB/s best-of but ~3.5-4.0 x10^3 per call in
-// the bench line. Workers are started once (grown on demand, never shrunk) and sleep
-// on a condition variable between calls; a call hands out job indices from an atomic
-// counter to its first n - 1 workers and the calling thread. One parallel call runs
-// at a time (calls from several host threads queue on run_mutex_). No exception
-// crosses the C ABI: a worker that cannot be started leaves its share to the others.
+// the bench line. Workers are started once (grown on demand up to the machine's
+// hardware threads, never shrunk) and sleep on a condition variable between calls; a
+// call hands out job indices from an atomic counter to its workers and the calling
+// thread, so a call asking for more threads than the cap still runs every job, on
+// fewer threads. One parallel call runs at a time (calls from several host threads
+// queue on run_mutex_). No exception crosses the C ABI: a worker that cannot be
+// started leaves its share to the others.
+//
+// fork(): the child inherits the pool's state but none of its threads. pthread_atfork
+// handlers take both mutexes before the fork (so no call is half-way through), release
+// them in the parent, and in the child forget the dead workers (their std::thread
+// objects are leaked: neither joining nor destroying a joinable thread is possible
+// there) and start from fresh mutexes and condition variables, so the child's first
+// call starts its own workers.
 class Pool {
  public:
+  Pool() : cap_(std::max(1u, std::thread::hardware_concurrency())) {
+    pthread_atfork(&Pool::prepare, &Pool::parent, &Pool::child);
+  }
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(m_);
@@ -161,7 +176,7 @@ class Pool {
   // fn(j) for j in [0, njobs) on up to `threads` threads (the caller included).
   void run(uint32_t threads, uint32_t njobs, const std::function<void(uint32_t)> &fn) {
     std::lock_guard<std::mutex> call(run_mutex_);
-    const uint32_t want = threads > 1 ? threads - 1 : 0;
+    const uint32_t want = std::min(threads, cap_) > 1 ? std::min(threads, cap_) - 1 : 0;
     try {
       while (workers_.size() < want) {
         const uint32_t id = (uint32_t)workers_.size();
@@ -185,6 +200,11 @@ class Pool {
     fn_ = nullptr;
   }
 
+  static Pool &get() {
+    static Pool p;
+    return p;
+  }
+
  private:
   void work() {
     for (uint32_t j; (j = next_.fetch_add(1, std::memory_order_relaxed)) < njobs_;) (*fn_)(j);
@@ -203,7 +223,32 @@ class Pool {
       if (--busy_ == 0) done_cv_.notify_one();
     }
   }
+  static void prepare() {
+    Pool &p = get();
+    p.run_mutex_.lock();
+    p.m_.lock();
+  }
+  static void parent() {
+    Pool &p = get();
+    p.m_.unlock();
+    p.run_mutex_.unlock();
+  }
+  static void child() {
+    Pool &p = get();
+    // the workers do not exist here: drop their handles without touching them
+    new std::vector<std::thread>(std::move(p.workers_));
+    p.workers_.clear();
+    p.active_ = p.busy_ = 0;
+    // fresh synchronisation objects: the condition variables' internal state still
+    // counts the parent's sleeping workers as waiters (a broadcast would wait for them
+    // to leave), and both mutexes are held by prepare()
+    new (&p.cv_) std::condition_variable();
+    new (&p.done_cv_) std::condition_variable();
+    new (&p.m_) std::mutex();
+    new (&p.run_mutex_) std::mutex();
+  }
 
+  const uint32_t cap_;
   std::mutex run_mutex_, m_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> workers_;
@@ -213,11 +258,6 @@ class Pool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
-
-Pool &pool() {
-  static Pool p;
-  return p;
-}
 
 }  // namespace
 
@@ -310,7 +350,7 @@ int mh_decode_frame_cpu(const uint32_t *block_offsets, const uint8_t *codes, uin
     const std::function<void(uint32_t)> job = [&](uint32_t j) {
       rows((uint32_t)((uint64_t)bh * j / nt), (uint32_t)((uint64_t)bh * (j + 1) / nt));
     };
-    pool().run(nt, nt, job);
+    Pool::get().run(nt, nt, job);
   } catch (...) {
     return MH_ERR_CAPACITY;  // no exception crosses the C ABI
   }

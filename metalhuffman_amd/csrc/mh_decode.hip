@@ -36,6 +36,9 @@ namespace {
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0        //    (scripts/diag_stamps.py)
 #endif
+#ifndef MH_LANE_PAIRS           // 1: the lane-pair diagnostic library only (libmh_diag_lanepairs.so,
+#define MH_LANE_PAIRS 0         //    metalhuffman_amd/build.py), which exports mh_diag_decode_lanepairs
+#endif
 constexpr int kStageBytes = 4352;             // per-wave LDS window (max tile span)
 constexpr int kMaxWavesPerWG = 8;             // batch kernel workgroup width
 constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = what the LDS budget admits
@@ -44,7 +47,6 @@ constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = wh
 // L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt).
 constexpr int kBatchStoreAux = 2;
 constexpr int kSmallStoreAux = 18;
-constexpr uint32_t kLpMinBits = 16;           // lane-pair variant: blocks shorter than 2x this decode on one lane
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
@@ -125,6 +127,7 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
 }
 
 
+#if !MH_LANE_PAIRS
 // mh_prepare_lut: the prepared tables from T1/T2 in device memory, one workgroup
 // (build_prepared_lut, mh_lut.hpp).
 __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1, const uint16_t *t2,
@@ -135,6 +138,7 @@ __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1
   __syncthreads();
   build_prepared_lut(s_t1, t2, t2_entries, buf, s_scratch);
 }
+#endif
 
 // Word source for the bit cursor: big-endian dwords of the tile's code span.
 struct LdsWords {
@@ -574,12 +578,93 @@ __device__ __forceinline__ void decode_halves(const DecodeArgs &a, const Tile &t
   (void)fbits;
 }
 
-// Persistent loop: wave w of workgroup g decodes tiles g*W + w, + gridDim*W, ...
-// Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
-// header of tile i+2 and the code span of tile i+1 are in flight into registers;
-// the span is written to the wave's LDS window once tile i has finished reading it.
+#if MH_DIAG_STAMPS
+#define MH_TS_PARAM , unsigned long long (&ts)[kDiagSlots]
+#define MH_TS_ARG , ts
+#else
+#define MH_TS_PARAM
+#define MH_TS_ARG
+#endif
+
+// static grid-stride schedule; a tile id >= total_tiles means "no tile"
+__device__ __forceinline__ uint32_t next_tile(const DecodeArgs &a, uint32_t t, uint32_t gstride) {
+  return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles;
+}
+
+// The batch kernel's persistent loop for ONE step flavour (Cfg), entered with the
+// first tile resolved and its span in flight (R), the second tile's header in flight
+// (hn). Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
+// header of tile i+2 and the code span of tile i+1 are in flight into registers; the
+// span is written to the wave's LDS window once tile i has finished reading it.
+// One instantiation per flavour: round 4 folded the three into one loop with a per-tile
+// flavour switch, and the batch and flat 8192^2 launches lost 9-11 % (VERDICT r04,
+// profiles/r05_bisect_ab.txt).
+template <bool kDelta, class Cfg>
+__device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, uint8_t *stage,
+                                           const uint8_t *lut, uint32_t gstride, Tile cur,
+                                           bool cur_staged, const TileHdr &hn0,
+                                           v4u32 (&R)[kStageChunks] MH_TS_PARAM) {
+  TileHdr hn = hn0;
+#if MH_DIAG_STAMPS
+  bool first_tile = true;
+#endif
+  if (cur_staged) span_write<Cfg::kSwz>(cur, lane, R, stage);
+  MH_STAMP(3);
+  // Resolved even past the end (zero-record loads): every Tile field is defined
+  // before span_issue builds a descriptor from it.
+  Tile nxt = hdr_resolve(a, hn, lane);
+
+  // Per iteration the only VMEM issued after a prefetch is the 8 unconditional row
+  // stores, so every wait below is an exact vmcnt that leaves the stores in flight.
+  while (cur.tile < a.total_tiles) {  // wave-uniform
+    if (__builtin_expect(!cur_staged, 0)) break;  // oversize span: finish in the slow loop
+    const bool nxt_live = nxt.tile < a.total_tiles;
+    const bool nxt_staged = nxt_live && nxt.span <= (uint32_t)kStageBytes;
+    span_issue(a, nxt, lane, R, nxt_staged);  // unconditional (all out of range if not staged)
+    hdr_issue(a, next_tile(a, nxt.tile, gstride), lane, hn);
+
+    wave_sync();  // this tile's staging writes -> reads
+    {
+      const bool dead = !cur.valid;
+      const OutTile ot = out_tile(a, cur, lane);
+      LdsWords src{stage};
+      // waves with more tiles left run first (the arbiter otherwise favours the oldest)
+      set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
+      decode_block<kDelta, Cfg>(src, lut, cur.p, cur.init, ot.rsrc, ot.row0, (uint32_t)a.out_pitch, dead);
+    }
+#if MH_DIAG_STAMPS
+    if (first_tile) MH_STAMP(4);
+    first_tile = false;
+#endif
+    wave_sync();  // this tile's reads -> next tile's staging writes
+    if (nxt_staged) span_write<Cfg::kSwz>(nxt, lane, R, stage);
+    const Tile nn = hdr_resolve(a, hn, lane);
+    cur = nxt;
+    cur_staged = nxt_staged;
+    nxt = nn;
+  }
+
+  // Slow loop (rare): a tile whose code span exceeds the LDS window (long codes in
+  // most of its 64 blocks) and every later tile of this wave, without prefetch.
+  // Kept after the pipelined loop so its waits never merge into that loop.
+  for (uint32_t t = cur.tile; t < a.total_tiles; t = next_tile(a, t, gstride)) {
+    __builtin_amdgcn_s_waitcnt(0);
+    TileHdr h;
+    hdr_issue(a, t, lane, h);
+    const Tile tt = hdr_resolve(a, h, lane);
+    const OutTile ot = out_tile(a, tt, lane);
+    decode_halves<kDelta, Cfg>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+  }
+}
+
+// The batch kernel: persistent workgroups (wave w of workgroup g decodes tiles
+// g*W + w, + grid*W, ...). A common prologue (table copy, first two headers, first
+// span) and then one instantiation of the persistent loop per step flavour, chosen
+// from the prepared table's code lengths (kernel-uniform): no code longer than 13 bits
+// -> escape-free; one code length only -> escape-free with the swizzled stage. An
+// in-kernel table (no prepared LUT) keeps the general step.
 template <bool kDelta>
-__device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
+__global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(const DecodeArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = a.nwaves;
@@ -589,12 +674,9 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   const uint8_t *lut = reinterpret_cast<const uint8_t *>(s_lut);
 #if MH_DIAG_STAMPS
   unsigned long long ts[kDiagSlots] = {};
-  bool first_tile = true;
 #endif
   MH_STAMP(0);
 
-  // static grid-stride schedule; a tile id >= total_tiles means "no tile"
-  const auto next_tile = [&](uint32_t t) { return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles; };
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr hc, hn;
   // ---- lookup table into LDS (shared by the workgroup) ----
@@ -618,8 +700,7 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   }
   hdr_issue(a, t0, lane, hc);
   // The step flavour, from the prepared table's code lengths (kernel-uniform): issued
-  // behind the first header, and only waited for at the first tile's decode, so no
-  // dependent load sits in front of the header (one flavour switch per tile).
+  // behind the first header, so no dependent load sits in front of it.
   //   2: one code length (flat) -> escape-free step, swizzled stage
   //   1: no code over 13 bits   -> escape-free step
   //   0: general step (escapes), also for an in-kernel table
@@ -642,11 +723,11 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   }
 
   v4u32 R[kStageChunks];
-  Tile cur = hdr_resolve(a, hc, lane);
+  const Tile cur = hdr_resolve(a, hc, lane);
   MH_STAMP(1);
-  bool cur_staged = cur.tile < a.total_tiles && cur.span <= (uint32_t)kStageBytes;
+  const bool cur_staged = cur.tile < a.total_tiles && cur.span <= (uint32_t)kStageBytes;
   span_issue(a, cur, lane, R, cur_staged);
-  hdr_issue(a, next_tile(t0), lane, hn);
+  hdr_issue(a, next_tile(a, t0, gstride), lane, hn);
 
   if (fixed_copy) {
     // (table in LDS, barrier passed above)
@@ -657,67 +738,12 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   }
   MH_STAMP(2);
   const uint32_t flavor = !a.lut ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
-  if (cur_staged) {
-    if (flavor == 2) span_write<true>(cur, lane, R, stage);
-    else span_write<false>(cur, lane, R, stage);
-  }
-  MH_STAMP(3);
-  // Resolved even past the end (zero-record loads): every Tile field is defined
-  // before span_issue builds a descriptor from it.
-  Tile nxt = hdr_resolve(a, hn, lane);
-
-  // Per iteration the only VMEM issued after a prefetch is the 8 unconditional row
-  // stores, so every wait below is an exact vmcnt that leaves the stores in flight.
-  while (cur.tile < a.total_tiles) {  // wave-uniform
-    if (__builtin_expect(!cur_staged, 0)) break;  // oversize span: finish in the slow loop
-    const bool nxt_live = nxt.tile < a.total_tiles;
-    const bool nxt_staged = nxt_live && nxt.span <= (uint32_t)kStageBytes;
-    span_issue(a, nxt, lane, R, nxt_staged);  // unconditional (all out of range if not staged)
-    hdr_issue(a, next_tile(nxt.tile), lane, hn);
-
-    wave_sync();  // this tile's staging writes -> reads
-    {
-      const bool dead = !cur.valid;
-      const OutTile ot = out_tile(a, cur, lane);
-      const __amdgpu_buffer_rsrc_t out = ot.rsrc;
-      const uint32_t row0 = ot.row0;
-      LdsWords src{stage};
-      // waves with more tiles left run first (the arbiter otherwise favours the oldest)
-      set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
-      if (flavor == 1)
-        decode_block<kDelta, Lut13NoEsc>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
-      else if (flavor == 2)
-        decode_block<kDelta, Lut13Flat>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
-      else
-        decode_block<kDelta, Lut13>(src, lut, cur.p, cur.init, out, row0, (uint32_t)a.out_pitch, dead);
-    }
-#if MH_DIAG_STAMPS
-    if (first_tile) MH_STAMP(4);
-    first_tile = false;
-#endif
-    wave_sync();  // this tile's reads -> next tile's staging writes
-    if (nxt_staged) {
-      if (flavor == 2) span_write<true>(nxt, lane, R, stage);
-      else span_write<false>(nxt, lane, R, stage);
-    }
-    const Tile nn = hdr_resolve(a, hn, lane);
-    cur = nxt;
-    cur_staged = nxt_staged;
-    nxt = nn;
-  }
-
-  // Slow loop (rare): a tile whose code span exceeds the LDS window (long codes in
-  // most of its 64 blocks) and every later tile of this wave, without prefetch.
-  // Kept after the pipelined loop so its waits never merge into that loop.
-  for (uint32_t t = cur.tile; t < a.total_tiles; t = next_tile(t)) {
-    __builtin_amdgcn_s_waitcnt(0);
-    TileHdr h;
-    hdr_issue(a, t, lane, h);
-    const Tile tt = hdr_resolve(a, h, lane);
-    const OutTile ot = out_tile(a, tt, lane);
-    if (flavor == 2) decode_halves<kDelta, Lut13Flat>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
-    else decode_halves<kDelta, Lut13>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
-  }
+  if (flavor == 1)
+    batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
+  else if (flavor == 2)
+    batch_loop<kDelta, Lut13Flat>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
+  else
+    batch_loop<kDelta, Lut13>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
   __builtin_amdgcn_s_waitcnt(0);
@@ -728,15 +754,6 @@ __device__ __forceinline__ void batch_tiles(const DecodeArgs &a) {
   if (lane == 0 && gw < (uint32_t)kDiagWaves)
     for (int i = 0; i < kDiagSlots; ++i) g_stamps[gw * kDiagSlots + i] = ts[i];
 #endif
-}
-
-// The batch kernel: one instantiation of the persistent loop per step flavour,
-// chosen from the prepared table's code lengths (kernel-uniform): no code longer
-// than 13 bits -> escape-free; one code length only -> escape-free with the
-// swizzled stage. An in-kernel table (no prepared LUT) keeps the general step.
-template <bool kDelta>
-__global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(const DecodeArgs a) {
-  batch_tiles<kDelta>(a);
 }
 
 // ---- small launches (<= one wave per SIMD, e.g. one 2048x1536 frame) -------------
@@ -832,6 +849,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 #endif
 }
 
+#if MH_LANE_PAIRS
 // ---- lane-pair variant of the small-launch kernel (MH_FLAG_LANE_PAIRS, A/B) -------
 // north_star's lane-group cursor: each 8x8 block is decoded by two lanes of one
 // wave, lanes l and l ^ 32 (32 blocks per wave, so twice the waves of the small
@@ -844,6 +862,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const
 // masks through three ds_bpermutes on every step and stored every symbol to LDS
 // (35.7 vs 5.8 us); this one runs the default step with register output and swaps
 // the window masks only at sparse checkpoints.
+constexpr uint32_t kLpMinBits = 16;  // blocks shorter than 2x this decode on one lane
 constexpr int kLpWaves = 4;
 constexpr int kLpStageBytes = 4144;   // >= 15 + 32 blocks x 64 x 16 bits / 8 + 24, 16-B multiple
 static_assert(kLpStageBytes <= kStageChunks * 64 * 16, "span_issue covers the lane-pair stage");
@@ -1144,6 +1163,8 @@ __global__ void __launch_bounds__(64 * kLpWaves) mh_decode_lanepair_kernel(const
                                                 spec, init, out, row0, (uint32_t)a.out_pitch);
 }
 
+#endif  // MH_LANE_PAIRS
+
 // Per-device launch parameters (CU count, batch-kernel occupancy per workgroup
 // size), computed once per device ordinal under a per-device mutex: no mutable state
 // is shared between devices or written by concurrent callers (the reference keeps
@@ -1213,6 +1234,7 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   const DeviceInfo *di = device_info(s);
   if (!di) return MH_ERR_HIP;
   const int cus = di->cus.load(std::memory_order_relaxed);
+#if MH_LANE_PAIRS
   if (lane_pairs && a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // experimental lane-pair decode (MH_FLAG_LANE_PAIRS): 32-block tiles
     const uint32_t n_frames = a.total_tiles / a.tiles_per_frame;
@@ -1222,6 +1244,9 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
     MH_LAUNCH(mh_decode_lanepair_kernel<kDelta>, dim3(a.n_groups), dim3(kLpWaves * 64), s, any_order, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
+#else
+  (void)lane_pairs;
+#endif
   if (a.lut && a.total_tiles <= (uint32_t)(kSmallMaxTilesPerCU * cus)) {
     // one tile per wave, kSmallWaves waves per workgroup: fewer workgroups copy the
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
@@ -1247,6 +1272,8 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
 }  // namespace
 
 extern "C" {
+
+#if !MH_LANE_PAIRS
 
 #if MH_DIAG_STAMPS
 int mh_diag_stamps(unsigned long long *host, size_t n) {
@@ -1282,12 +1309,22 @@ int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_t
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
+#endif  // !MH_LANE_PAIRS
+
+// The decode entry point. The lane-pair diagnostic library exports the same body as
+// mh_diag_decode_lanepairs (and nothing else): MH_FLAG_LANE_PAIRS is honoured only there.
+#if MH_LANE_PAIRS
+int mh_diag_decode_lanepairs(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_frame_stride,
+                             void *stream) {
+#else
 int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_frame_stride,
               void *stream) {
+#endif
   if (!fr || !d_out || !fr->d_block_offsets || !fr->d_codes || !fr->d_table1 || !fr->d_table2)
     return MH_ERR_INVALID_ARG;
   if (fr->n_frames == 0 || (fr->n_frames > 1 && !fr->d_frame_code_offsets)) return MH_ERR_INVALID_ARG;
-  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_LANE_PAIRS | MH_FLAG_ANY_ORDER)) return MH_ERR_INVALID_ARG;
+  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_ANY_ORDER | (MH_LANE_PAIRS ? MH_FLAG_LANE_PAIRS : 0u)))
+    return MH_ERR_INVALID_ARG;
   const mh_dims &d = fr->dims;
   if (!d.width || !d.height || d.width > MH_MAX_DIM || d.height > MH_MAX_DIM ||
       d.block_width != (d.width + 7) / 8 || d.block_height != (d.height + 7) / 8)

@@ -176,6 +176,15 @@ __device__ __forceinline__ uint64_t row_symbols(uint64_t q, uint32_t r, bool del
 // hist and tile_hist slices).
 constexpr uint32_t kTileGroups = kCodeTile / 32;
 static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgroup's batch covers a code tile");
+// Blocks per tile of the batched path (split workgroup, tree tile counts, packer wave).
+// Bigger tiles halve the per-tile records (counts, offsets, last-block symbols) the
+// split writes and the trees read; A/B builds set MH_BATCH_TILE.
+#ifndef MH_BATCH_TILE
+#define MH_BATCH_TILE 128
+#endif
+constexpr uint32_t kBatchTile = MH_BATCH_TILE;
+static_assert(kBatchTile / 32 <= kSplitBatch && kBatchTile % 32 == 0 && kBatchTile * 64 < 65536,
+              "a split workgroup's batch covers a batch tile; u16 tile counts");
 
 // Row r of this lane's block (32 g + lane / 8) of group g as ONE unconditional buffer
 // load (kVec: 8 bytes; else 8 byte loads), zero past the frame: a fixed count of loads
@@ -220,7 +229,7 @@ __device__ __forceinline__ uint64_t group_row(const uint8_t *gray, uint32_t W, u
 // block tb, row r, from one descriptor at the tile's first block row. The tile's
 // coordinates are uniform (one scalar division); a lane's block wraps into the next
 // block row at most once when the frame is >= kCodeTile blocks wide.
-template <bool kVec, uint32_t N>
+template <bool kVec, uint32_t N, uint32_t kTile>
 __device__ __forceinline__ void tile_rows(const uint8_t *gray, uint32_t W, uint32_t H, uint32_t bw, uint64_t nb,
                                           uint32_t tb, uint32_t r, uint64_t (&q)[N]) {
   // no 64-bit compares and no per-load v_mul_lo (quarter rate): 32-bit block indices
@@ -234,7 +243,7 @@ __device__ __forceinline__ void tile_rows(const uint8_t *gray, uint32_t W, uint3
 #pragma unroll
   for (uint32_t u = 0; u < N; ++u) {
     uint32_t bx = tbx + k + 32u * u, dy = 0, doff = 0;
-    if (bw >= kCodeTile) {
+    if (bw >= kTile) {
       const bool wrap = bx >= bw;
       bx = wrap ? bx - bw : bx;
       dy = wrap ? 8u : 0u;
@@ -262,12 +271,13 @@ __device__ __forceinline__ void tile_rows(const uint8_t *gray, uint32_t W, uint3
   }
 }
 
-template <bool kVec, bool kTiled>
+template <bool kVec, bool kTiled, uint32_t kTile = kCodeTile>
 __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uint32_t W, uint32_t H,
                                                         uint32_t bw, uint64_t nb, uint32_t flags,
                                                         uint8_t *sym, uint8_t *block_init,
                                                         uint64_t *hist, uint16_t *tile_hist, uint64_t *meta,
-                                                        uint32_t ncode, uint64_t gray_stride) {
+                                                        uint32_t ncode, uint64_t gray_stride,
+                                                        uint64_t *tile_tail) {
   constexpr bool tiled = kTiled;
   uint32_t wg = blockIdx.x;  // tiled: this frame's tile
   if (tiled) {
@@ -277,6 +287,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
     if (block_init) block_init += (uint64_t)f * nb;
     if (hist) hist += (uint64_t)f * kHistParts * 256;
     tile_hist += (uint64_t)f * ncode * 256;
+    if (tile_tail) tile_tail += (uint64_t)f * ncode * 8;
   }
   if (tiled && meta && blockIdx.x == 0 && threadIdx.x == 0) {  // the code kernel runs after this one
     meta[kFlag] = 0;
@@ -313,6 +324,10 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
         if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
       }
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+      // batched path: the tile's last block's symbols, for the next tile's packer (its
+      // first code word starts with this block's last bits); 64 B per tile instead of
+      // the packer re-reading the block's eight pixel rows (eight 128-B lines) from HBM
+      if (tiled && tile_tail && (uint32_t)b == wg * kTile + (kTile - 1u)) tile_tail[(uint64_t)wg * 8u + r] = v;
     }
   };
   // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
@@ -320,13 +335,14 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint64_t ngroups = (nb + 31) / 32;
   // grid-stride over groups, or (tiled) one batch of consecutive groups
   const uint64_t ustep = tiled ? 1u : gridDim.x;
-  const uint64_t gfirst = tiled ? (uint64_t)wg * kTileGroups : blockIdx.x;
+  constexpr uint32_t kGroups = kTile / 32;  // tiled: groups of 32 blocks per tile
+  const uint64_t gfirst = tiled ? (uint64_t)wg * kGroups : blockIdx.x;
   const uint64_t gstride = tiled ? ngroups : (uint64_t)kSplitBatch * gridDim.x;
   for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
-    constexpr uint32_t nu = kTiled ? kTileGroups : kSplitBatch;
+    constexpr uint32_t nu = kTiled ? kGroups : kSplitBatch;
     uint64_t q[nu];
     if constexpr (kTiled) {
-      tile_rows<kVec>(gray, W, H, bw, nb, (uint32_t)g0 * 32u, r, q);
+      tile_rows<kVec, nu, kTile>(gray, W, H, bw, nb, (uint32_t)g0 * 32u, r, q);
     } else {
 #pragma unroll
       for (uint32_t u = 0; u < nu; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * ustep, r);
@@ -347,7 +363,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   lds_barrier();
   uint32_t c = 0;
   for (uint32_t k = 0; k < kHistCopies; ++k) c += h[threadIdx.x * kHistCopies + ((k + threadIdx.x) % kHistCopies)];
-  if (tiled) tile_hist[(uint64_t)wg * 256 + threadIdx.x] = (uint16_t)c;  // <= kCodeTile * 64
+  if (tiled) tile_hist[(uint64_t)wg * 256 + threadIdx.x] = (uint16_t)c;  // <= kTile * 64
   MH_SPLIT_STAMP(3)
   // kHistParts partial histograms (workgroups round-robin over them, as over the
   // XCDs): one address per bin would serialise every workgroup's atomic on it
@@ -1340,7 +1356,8 @@ __device__ __forceinline__ void wave_sync() {
 template <bool kVec, bool kPair>
 __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     const Pixels px, uint64_t gray_stride, uint64_t nb, uint32_t ncode, const uint32_t *table, const uint64_t *meta,
-    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t ncode_wg) {
+    const uint32_t *tile_off, uint32_t *offsets, uint8_t *codes, uint64_t codes_stride, uint32_t ncode_wg,
+    const uint64_t *tile_tail) {
   // ncode_wg: workgroups per frame (ncode rounded up to kPackWaves tiles): a workgroup's
   // waves pack tiles of ONE frame and share its table, at a fixed LDS address (the
   // gathers need no per-wave base: one VALU per symbol for the address)
@@ -1361,11 +1378,11 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   uint32_t *lw = s_w[wave];
   const uint32_t E = tile_off[(uint64_t)f * (ncode + 1) + t];
   const uint8_t *gray = px.gray + f * gray_stride;
-  const uint64_t b0 = (uint64_t)t * kCodeTile;
-  const uint32_t nsteps = (uint32_t)((min<uint64_t>(kCodeTile, nb - b0) + kStepBlocks - 1) / kStepBlocks);
+  const uint64_t b0 = (uint64_t)t * kBatchTile;
+  const uint32_t nsteps = (uint32_t)((min<uint64_t>(kBatchTile, nb - b0) + kStepBlocks - 1) / kStepBlocks);
   const uint32_t by0 = (uint32_t)(b0 / px.bw), bx0 = (uint32_t)(b0 - (uint64_t)by0 * px.bw);
-  // one descriptor from the block row before the tile's first: 32-bit offsets for any frame
-  const uint32_t yb = by0 ? (by0 - 1u) * 8u : 0u;
+  // one descriptor from the tile's first block row: 32-bit offsets for any frame
+  const uint32_t yb = by0 * 8u;
   const __amdgpu_buffer_rsrc_t rg = enc_rsrc(gray + (uint64_t)yb * px.W, (uint64_t)(px.H - yb) * px.W);
   // row r of block (bx + k, by) wrapped into the frame, zero when !live or past the frame
   // (32-bit block indices, nb < 2^26; the step's row offset uniform, r * W per lane
@@ -1404,13 +1421,14 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   uint32_t first_unused;
   // the tile's first word starts with the previous block's last E % 32 bits: lanes 0-7
   // recompute that block's codes (the previous tile leaves the shared word to this one)
+  // from its symbols, which the split kept for this (tile_tail: one 64-B read)
   uint32_t head = 0;
   const uint32_t r0 = E & 31u;
   if (r0) {  // wave-uniform; t > 0 here (tile 0 starts at bit 0)
-    const uint32_t pbx = bx0 ? bx0 - 1u : px.bw - 1u, pby = bx0 ? by0 : by0 - 1u;
-    const uint64_t qp = row_symbols(load_row(pbx, pby, (uint32_t)b0 - 1u, 0, lane, lane * px.W, lane < 8), lane & 7u,
-                                    px.delta, px.init_byte,
-                                    &first_unused);
+    const __amdgpu_buffer_rsrc_t rt = enc_rsrc(tile_tail + ((uint64_t)f * ncode + t - 1u) * 8u, 64u);
+    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+    const v2u32 tv = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(lane < 8 ? lane * 8u : kOob), 0, 0);
+    const uint64_t qp = ((uint64_t)tv.y << 32) | tv.x;
     uint32_t lenp = 0;
     uint64_t acc = 0;
 #pragma unroll
@@ -1563,10 +1581,11 @@ struct BatchWorkspace {  // per-frame slices, each part 256-B aligned; nothing n
   uint64_t *meta;       // n x kMetaWords
   uint16_t *tile_hist;  // n x ncode x 256
   uint32_t *tile_off;   // n x (ncode + 1)
+  uint64_t *tile_tail;  // n x ncode x 8: the symbols of each tile's last block (rows as u64)
 };
 
 uint64_t carve_batch(uint8_t *base, uint64_t nb, uint32_t n, BatchWorkspace *w) {
-  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  const uint64_t ncode = (nb + kBatchTile - 1) / kBatchTile;
   uint64_t o = 0;
   if (w) w->table = reinterpret_cast<uint32_t *>(base + o);
   o += align256((uint64_t)n * 256 * 4);
@@ -1576,6 +1595,8 @@ uint64_t carve_batch(uint8_t *base, uint64_t nb, uint32_t n, BatchWorkspace *w) 
   o += align256((uint64_t)n * ncode * 256 * 2);
   if (w) w->tile_off = reinterpret_cast<uint32_t *>(base + o);
   o += align256((uint64_t)n * (ncode + 1) * 4);
+  if (w) w->tile_tail = reinterpret_cast<uint64_t *>(base + o);
+  o += align256((uint64_t)n * ncode * 64);
   return o;
 }
 
@@ -1665,7 +1686,8 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   if (ncode <= kFusedMaxTiles && path == 2) {
     // two launches: the tiled split, then tree + offsets + packing in one kernel
     hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3((uint32_t)ncode),
-                       dim3(256), 0, s, d_gray, width, height, bw, nb, flags, nullptr, d_block_init, w.hist, w.tile_hist, w.meta, (uint32_t)ncode, 0ull);
+                       dim3(256), 0, s, d_gray, width, height, bw, nb, flags, nullptr, d_block_init, w.hist, w.tile_hist, w.meta, (uint32_t)ncode, 0ull,
+                       nullptr);
     const Pixels px{d_gray, width, height, bw, vec, !(flags & MH_FLAG_NO_DELTA), d_block_init != nullptr};
     hipLaunchKernelGGL(enc_code_kernel, dim3((uint32_t)ncode + 1), dim3(kCodeThreads), 0, s, w.hist,
                        d_canon_header, w.table, w.meta, d_codes_len, codes_cap, d_status, px, w.tile_hist, nb,
@@ -1674,7 +1696,7 @@ int mh_encode_frame_device_async(const uint8_t *d_gray, uint32_t width, uint32_t
   }
   const uint32_t gsplit = (uint32_t)std::min<uint64_t>((nb + 31) / 32, kSplitWgs);
   hipLaunchKernelGGL((vec ? enc_split_kernel<true, false> : enc_split_kernel<false, false>), dim3(gsplit), dim3(256), 0,
-                     s, d_gray, width, height, bw, nb, flags, w.sym, d_block_init, w.hist, nullptr, w.meta, 0u, 0ull);
+                     s, d_gray, width, height, bw, nb, flags, w.sym, d_block_init, w.hist, nullptr, w.meta, 0u, 0ull, nullptr);
   hipLaunchKernelGGL(enc_tree_kernel, dim3(1), dim3(kTreeThreads), 0, s, w.hist, d_canon_header, w.table, w.meta,
                      d_codes_len, codes_cap, d_status, nb * 64);
   hipLaunchKernelGGL(enc_scan_kernel, dim3((uint32_t)ntiles), dim3(kScanTile), 0, s, w.sym, w.table, nb, w.blen,
@@ -1730,7 +1752,7 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
   if (gray_frame_stride < (uint64_t)width * height && n_frames > 1) return MH_ERR_CAPACITY;
   const uint32_t bw = (width + 7) / 8, bh = (height + 7) / 8;
   const uint64_t nb = (uint64_t)bw * bh;
-  const uint64_t ncode = (nb + kCodeTile - 1) / kCodeTile;
+  const uint64_t ncode = (nb + kBatchTile - 1) / kBatchTile;
   if (ncode * n_frames > 0x7FFFFFFFull || n_frames > 0x7FFFFFFFu) return MH_ERR_CAPACITY;
   if (workspace_bytes < mh_encode_frames_workspace_bytes(width, height, n_frames)) return MH_ERR_CAPACITY;
   BatchWorkspace w;
@@ -1752,9 +1774,11 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
     uint32_t *to = w.tile_off + (uint64_t)f0 * (ncode + 1);
     // one workgroup per tile (a persistent split with the next tile's rows in flight
     // measured slower: profiles/r04_v4_encoder_batch_ab.txt)
-    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true> : enc_split_kernel<false, true>), dim3(nt), dim3(256), 0, st,
+    uint64_t *tail = w.tile_tail + (uint64_t)f0 * ncode * 8;
+    hipLaunchKernelGGL((vec ? enc_split_kernel<true, true, kBatchTile> : enc_split_kernel<false, true, kBatchTile>), dim3(nt),
+                       dim3(256), 0, st,
                        gray, width, height, bw, nb, flags, nullptr, binit, nullptr, th, nullptr, (uint32_t)ncode,
-                       gray_frame_stride);
+                       gray_frame_stride, tail);
     hipLaunchKernelGGL(enc_tree_batch_kernel, dim3(m), dim3(kTreeThreads), 0, st, nullptr,
                        d_canon_headers + (uint64_t)f0 * 256, table, meta, d_codes_len ? d_codes_len + f0 : nullptr,
                        codes_frame_stride, d_status ? d_status + f0 : nullptr, nb, th, (uint32_t)ncode, to,
@@ -1766,7 +1790,7 @@ int mh_encode_frames_device_async(const uint8_t *d_gray, uint64_t gray_frame_str
                             : bw % 2 ? enc_pack_wave_kernel<true, false> : enc_pack_wave_kernel<true, true>),
                        dim3(ncode_wg * m), dim3(kPackWaves * 64), 0, st, px, gray_frame_stride, nb, (uint32_t)ncode, table,
                        meta, to, d_block_offsets + (uint64_t)f0 * nb, d_codes + f0 * codes_frame_stride,
-                       codes_frame_stride, ncode_wg);
+                       codes_frame_stride, ncode_wg, tail);
   };
   // One sub-batch: splitting the call into sub-batches alternated over a second stream
   // (trees beside another sub-batch's split / packing) measured slower, and the packer's

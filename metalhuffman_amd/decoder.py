@@ -191,7 +191,8 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tensor] = None,
            stream: Optional[torch.cuda.Stream] = None, extra_flags: int = 0) -> torch.Tensor:
     """Decode every frame into out[n, H, pitch] (pitch = W rounded up to 8).
-    extra_flags: decode-only flags ORed into the frame's (MH_FLAG_LANE_PAIRS, MH_FLAG_ANY_ORDER).
+    extra_flags: decode-only flags ORed into the frame's (MH_FLAG_ANY_ORDER; MH_FLAG_LANE_PAIRS
+    routes the call to the lane-pair diagnostic library, _native.diag_lanepairs()).
     The per-call host path is kept lean (a cached struct, the raw current stream): one
     frame decodes in ~5.3 us, so every microsecond of Python shows in eager loops."""
     fr, dev_index = _frame_entry(frames, tables, extra_flags)
@@ -212,7 +213,10 @@ def decode(frames: DeviceFrames, tables: DeviceTables, out: Optional[torch.Tenso
         sp = _raw_stream(dev_index)
     else:
         sp = torch.cuda.current_stream(dev_index).cuda_stream
-    rc = N.lib().mh_decode(ctypes.byref(fr), out.data_ptr(), pitch, h * pitch, sp)
+    if fr.flags & N.MH_FLAG_LANE_PAIRS:  # the diagnostic library's kernel (A/B only)
+        rc = N.diag_lanepairs().mh_diag_decode_lanepairs(ctypes.byref(fr), out.data_ptr(), pitch, h * pitch, sp)
+    else:
+        rc = N.lib().mh_decode(ctypes.byref(fr), out.data_ptr(), pitch, h * pitch, sp)
     if rc:
         N.check(rc, "mh_decode")
     return out

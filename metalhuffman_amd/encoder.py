@@ -209,11 +209,26 @@ class AsyncEncodedBatch:
     block_init: Optional[torch.Tensor]
     flags: int
 
-    def frames(self) -> DeviceFrames:
-        """All slots as one DeviceFrames batch (valid when the frames share a table)."""
+    def frames(self, check: bool = True) -> DeviceFrames:
+        """All slots as one DeviceFrames batch (valid when the frames share a table).
+
+        check=True (default) synchronises once: it raises MHError if any frame was
+        rejected (that frame's slot and block offsets were never written, so decoding
+        the batch would read garbage), and `code_bytes` is the batch's payload bytes
+        (sum of codes_len minus the pads), as for DeviceFrames.pack. check=False stays
+        asynchronous: the caller must check `status` before trusting a decode of the
+        batch, and `code_bytes` is then the slots' capacity (n * slot minus the pads),
+        an upper bound of the payload."""
+        if check:
+            st = self.status.cpu()
+            bad = [i for i in range(self.n_frames) if int(st[i])]
+            if bad:
+                raise N.MHError(int(st[bad[0]]), f"mh_encode_frames_device_async: frame(s) {bad[:8]} rejected")
+            payload = int(self.codes_len.sum().item()) - self.n_frames * N.MH_CODES_PAD
+        else:
+            payload = int(self.codes.numel()) - self.n_frames * N.MH_CODES_PAD
         return DeviceFrames(self.width, self.height, self.n_frames, self.block_offsets, self.codes,
-                            self.frame_code_offsets, self.block_init, self.flags,
-                            int(self.codes.numel()) - self.n_frames * N.MH_CODES_PAD)
+                            self.frame_code_offsets, self.block_init, self.flags, payload)
 
     def frame(self, f: int) -> DeviceEncodedFrame:
         """Frame f (synchronises; raises MHError on a rejected frame)."""

@@ -69,6 +69,7 @@ def _frame(**kw):
     (dict(d_codes=None), -1),
     (dict(flags=0x80), -1),
     (dict(flags=0x8), -1),                                     # first unassigned flag bit
+    (dict(flags=0x2), -1),                                     # lane pairs: diagnostic library only
     (dict(n_frames=0), -1),
     (dict(n_frames=2), -1),                                    # batch without frame offsets
     (dict(table2_entries=100), -5),
@@ -128,6 +129,28 @@ def test_decode_rejects_bad_dims_and_pitch(mh):
     assert L.mh_check(ctypes.byref(_frame(dims=N.mh_dims(2048, 1536, 255, 192))), 0x70000, None) == -2
     assert L.mh_check(ctypes.byref(_frame(table2_entries=100)), 0x70000, None) == -5
     assert L.mh_check(ctypes.byref(_frame()), 0x70002, None) == -6
+
+
+def test_lane_pair_kernel_only_in_diagnostic_library(mh):
+    """the lane-pair kernel (a measured negative kept for A/B) is not
+    in the product library; the diagnostic library carries it behind its one entry point,
+    which validates like mh_decode and accepts MH_FLAG_LANE_PAIRS."""
+    import metalhuffman_amd.build as B
+    from metalhuffman_amd import _native as N
+    B.build_diag()
+    prod = subprocess.run(["nm", "-D", "--defined-only", mh.LIB_PATH], check=True, capture_output=True,
+                          text=True).stdout
+    assert "lanepair" not in prod and "lanepair" not in open(mh.LIB_PATH, "rb").read().decode("latin-1")
+    diag = B.diag_lib_path("lanepairs")
+    syms = subprocess.run(["nm", "-D", "--defined-only", diag], check=True, capture_output=True,
+                          text=True).stdout
+    exported = sorted(l.split()[-1] for l in syms.splitlines() if " T " in l)
+    assert exported == ["mh_build_stamp", "mh_diag_decode_lanepairs"], exported
+    assert "lanepair_kernel" in open(diag, "rb").read().decode("latin-1")
+    L = N.diag_lanepairs()
+    assert L.mh_diag_decode_lanepairs(ctypes.byref(_frame(flags=0x8)), 0x50000, 2048, 0, None) == -1
+    assert L.mh_diag_decode_lanepairs(ctypes.byref(_frame(codes_bytes=2, flags=0x2)), 0x50000, 2048, 0,
+                                      None) == -4
 
 
 def test_constants(mh):

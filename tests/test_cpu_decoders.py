@@ -98,3 +98,45 @@ def test_argument_errors(mh):
     with pytest.raises(mh.MHError):
         mh.Huffman.decodeHuffmanBitsFromTables(t1, t2, 9, 7, 4, np.zeros(16, np.uint8))
     del out
+
+
+def test_frame_decoder_pool_survives_fork(mh, bigbridge):
+    """the persistent worker pool is fork-safe. The parent decodes
+    on 4 threads (workers started), forks, and the child decodes on 4 threads again: its
+    pool forgets the parent's workers (which do not exist in the child) and starts its
+    own, instead of waiting forever for them. A parent decode after the fork still works."""
+    import os
+    ef = mh.encode_frame(np.ascontiguousarray(bigbridge[:512, :1024]))
+    want = np.ascontiguousarray(bigbridge[:512, :1024])
+    assert np.array_equal(mh.decode_frame_cpu(ef, 4), want)
+    pid = os.fork()
+    if pid == 0:  # child: exit code says whether it decoded correctly
+        code = 1
+        try:
+            ok = np.array_equal(mh.decode_frame_cpu(ef, 4), want)
+            ok = ok and np.array_equal(mh.decode_frame_cpu(ef, 7), want)
+            code = 0 if ok else 2
+        finally:
+            os._exit(code)
+    import time
+    deadline = time.time() + 60
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() > deadline:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            pytest.fail("child decode hung after fork")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    assert np.array_equal(mh.decode_frame_cpu(ef, 4), want)
+
+
+def test_frame_decoder_more_threads_than_cap(mh, bigbridge):
+    """A call asking for more threads than the machine has runs every job on the
+    capped pool (jobs are handed out from a counter)."""
+    import os
+    ef = mh.encode_frame(np.ascontiguousarray(bigbridge[:1024, :512]))
+    n = 4 * (os.cpu_count() or 8)
+    assert np.array_equal(mh.decode_frame_cpu(ef, n), np.ascontiguousarray(bigbridge[:1024, :512]))

@@ -154,6 +154,10 @@ def test_bench_dist_path_on_rccl_world1():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["frames_verified"] == 8 and line["ranks_verified"] == 1
+    rd = line["rank_devices"]  # the line names each rank's GPU
+    assert rd["backend"] == "nccl" and rd["distinct_devices"] == 1, rd
+    assert rd["devices"][0]["rank"] == 0 and rd["devices"][0]["ordinal"] == 0, rd
+    assert rd["devices"][0]["pci"].count(":") >= 2, rd
     assert line["table_broadcast_bytes"] == 256
     ex = line["extras"]
     assert ex["config4"]["frames_verified_rank0"] == 8

@@ -57,7 +57,9 @@ def test_batch_64_bigbridge_shuffles_decode_as_one_batch(mh, device, bigbridge):
     canon = a.canon.cpu().numpy()
     assert all(np.array_equal(canon[0], c) for c in canon)  # block shuffles share the table
     t1, t2 = mh.Huffman.generateSplitLookupTables(canon[0])
-    out = D.decode(a.frames(), D.DeviceTables.upload(t1, t2, device))
+    fr = a.frames()
+    assert fr.code_bytes == int(a.codes_len.sum().item()) - 64 * mh.MH_CODES_PAD  # payload bytes
+    out = D.decode(fr, D.DeviceTables.upload(t1, t2, device))
     torch.cuda.synchronize(device)
     assert torch.equal(out[..., :2048], torch.from_numpy(np.stack(imgs)).to(device))
 
@@ -90,7 +92,12 @@ def test_batch_mixed_histograms_and_rejected_frame(mh, device, bigbridge):
             image_from_block_deltas(fibonacci_deltas(15, h * w, seed=4), w, h),
             image_from_block_deltas(fibonacci_deltas(19, h * w, seed=2), w, h),  # depth > 16
             np.where(np.arange(h * w).reshape(h, w) % 3 == 0, 7, 0).astype(np.uint8)]
-    _check_batch(mh, device, imgs, expect_bad=(3,))
+    a = _check_batch(mh, device, imgs, expect_bad=(3,))
+    # a batch holding a rejected frame is not handed to decode silently
+    with pytest.raises(mh.MHError):
+        a.frames()
+    fr = a.frames(check=False)  # asynchronous: code_bytes is the slots' capacity
+    assert fr.code_bytes == a.codes.numel() - len(imgs) * mh.MH_CODES_PAD
 
 
 @pytest.mark.parametrize("hw", [(1, 1), (9, 17), (1001, 777), (8, 4096), (2056, 2048),

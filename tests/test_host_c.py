@@ -112,6 +112,12 @@ def test_multi_host_rccl_world1(multi_bin, bigbridge, tmp_path):
     assert line.startswith("multi ok 1 devices 64 frames_per_device 2048 1536"), r.stdout
     mbps = float(line.split("MBps_events ")[1].split()[0])
     assert mbps > 1e5, r.stdout  # a 64-frame launch decodes >> 1e5 MB/s on one MI355X
+    # self-proving run: one line per device with its HIP ordinal and
+    # PCI bus id, and the count of distinct devices that took part
+    devs = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("device ")]
+    assert len(devs) == 1 and devs[0][2:4] == ["ordinal", "0"] and devs[0][4] == "pci", r.stdout
+    assert devs[0][5].count(":") >= 2 and devs[0][-1] == "ok", r.stdout
+    assert line.split()[-2:] == ["devices_verified", "1"], line
 
 
 @pytest.mark.gpu
