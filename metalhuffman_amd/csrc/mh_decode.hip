@@ -591,23 +591,36 @@ __device__ __forceinline__ uint32_t next_tile(const DecodeArgs &a, uint32_t t, u
   return t < a.total_tiles ? min(t + gstride, a.total_tiles) : a.total_tiles;
 }
 
-// The batch kernel's persistent loop for ONE step flavour (Cfg), entered with the
-// first tile resolved and its span in flight (R), the second tile's header in flight
-// (hn). Software-pipelined one tile ahead: while tile i decodes (LDS + VALU only), the
-// header of tile i+2 and the code span of tile i+1 are in flight into registers; the
-// span is written to the wave's LDS window once tile i has finished reading it.
-// One instantiation per flavour: round 4 folded the three into one loop with a per-tile
-// flavour switch, and the batch and flat 8192^2 launches lost 9-11 % (VERDICT r04,
-// profiles/r05_bisect_ab.txt).
+// The batch kernel's persistent loop for ONE step flavour (Cfg), entered with the first
+// tile's header in flight (hc) and, when `synced`, the table in LDS. Software-pipelined
+// one tile ahead: while tile i decodes (LDS + VALU only), the header of tile i+2 and the
+// code span of tile i+1 are in flight into registers; the span is written to the wave's
+// LDS window once tile i has finished reading it. One instantiation per flavour, entered
+// with nothing but the first header live (a flavour branch with the first span in
+// flight spilled: 80 VGPRs + 40 B of scratch).
 template <bool kDelta, class Cfg>
 __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, uint8_t *stage,
-                                           const uint8_t *lut, uint32_t gstride, Tile cur,
-                                           bool cur_staged, const TileHdr &hn0,
-                                           v4u32 (&R)[kStageChunks] MH_TS_PARAM) {
-  TileHdr hn = hn0;
+                                           const uint8_t *lut, uint32_t t0, uint32_t gstride,
+                                           const TileHdr &hc, bool synced MH_TS_PARAM) {
+  TileHdr hn;
 #if MH_DIAG_STAMPS
   bool first_tile = true;
 #endif
+  v4u32 R[kStageChunks];
+  Tile cur = hdr_resolve(a, hc, lane);
+  MH_STAMP(1);
+  bool cur_staged = cur.tile < a.total_tiles && cur.span <= (uint32_t)kStageBytes;
+  span_issue(a, cur, lane, R, cur_staged);
+  hdr_issue(a, next_tile(a, t0, gstride), lane, hn);
+  if constexpr (Cfg::kEsc) {  // the general flavour: also an in-kernel table, or a copy loop
+    if (!synced) {
+      if (a.lut)
+        __syncthreads();
+      else
+        build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, a.nwaves * 64u, [] { __syncthreads(); });
+    }
+  }
+  MH_STAMP(2);
   if (cur_staged) span_write<Cfg::kSwz>(cur, lane, R, stage);
   MH_STAMP(3);
   // Resolved even past the end (zero-record loads): every Tile field is defined
@@ -678,7 +691,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   MH_STAMP(0);
 
   const uint32_t t0 = min(blockIdx.x * nwaves + wave, a.total_tiles);
-  TileHdr hc, hn;
+  TileHdr hc;
   // ---- lookup table into LDS (shared by the workgroup) ----
   // A fixed count of unconditional 16-B loads per thread (chunks past the table fall
   // outside the descriptor and return 0), issued FIRST, all in flight together; the
@@ -722,28 +735,14 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
     for (uint32_t i = threadIdx.x; i < kLutChunks; i += nthreads) dstv[i] = src[i];
   }
 
-  v4u32 R[kStageChunks];
-  const Tile cur = hdr_resolve(a, hc, lane);
-  MH_STAMP(1);
-  const bool cur_staged = cur.tile < a.total_tiles && cur.span <= (uint32_t)kStageBytes;
-  span_issue(a, cur, lane, R, cur_staged);
-  hdr_issue(a, next_tile(a, t0, gstride), lane, hn);
-
-  if (fixed_copy) {
-    // (table in LDS, barrier passed above)
-  } else if (a.lut) {
-    __syncthreads();
-  } else {
-    build_lut(a.t1, a.t2, a.t2_entries, s_lut, &s_p0, threadIdx.x, nthreads, [] { __syncthreads(); });
-  }
-  MH_STAMP(2);
-  const uint32_t flavor = !a.lut ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
+  // the escape-free flavours need a prepared table, so a full fixed copy (>= 5 waves)
+  const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
   if (flavor == 1)
-    batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
+    batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
-    batch_loop<kDelta, Lut13Flat>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
+    batch_loop<kDelta, Lut13Flat>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else
-    batch_loop<kDelta, Lut13>(a, lane, stage, lut, gstride, cur, cur_staged, hn, R MH_TS_ARG);
+    batch_loop<kDelta, Lut13>(a, lane, stage, lut, t0, gstride, hc, fixed_copy MH_TS_ARG);
 #if MH_DIAG_STAMPS
   MH_STAMP(5);
   __builtin_amdgcn_s_waitcnt(0);

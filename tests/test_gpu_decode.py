@@ -320,6 +320,39 @@ def test_batch_kernel_flat_table(mh, oracle, device):
     assert np.array_equal(out[3], _oracle_decode(oracle, efs[3]))
 
 
+@pytest.mark.parametrize("kind", ["flat", "noesc", "general"])
+def test_batch_kernel_multi_tile_waves_per_flavour(mh, device, bigbridge, kind):
+    """Every step flavour of the batch kernel (one persistent-loop instantiation each)
+    through its pipelined multi-tile loop: more tiles than resident waves (256 CUs x 24
+    waves), so waves decode 2+ tiles with the next span in flight. flat: uniform random
+    bytes (every code 8 bits, swizzled stage); noesc: the 8192-wide mirror tile (longest
+    code 13 bits); general: BigBridge shuffles (14-bit codes, escape test). The round-5
+    bisect found a flat-flavour failure here that no 1-tile-per-wave test could see."""
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import frames as F
+    if kind == "flat":
+        base = F.uniform_random(1024, 1024, 91)
+    elif kind == "noesc":
+        base = F.mirror_tile(bigbridge, 2048, 8192)
+    else:
+        base = np.ascontiguousarray(bigbridge[:1024, :1024])
+    n = max(1, -(-8400 * 64 // (base.size // 64)))  # > 8,192 tiles of 64 blocks
+    imgs = [base] + [F.block_shuffle(base, 500 + s) for s in range(n - 1)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    mx = int(efs[0].canon.max())
+    assert {"flat": mx == efs[0].canon[efs[0].canon > 0].min() == 8, "noesc": mx <= 13,
+            "general": mx > 13}[kind], mx
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    fr = D.DeviceFrames.pack(efs, device)
+    out = D.decode(fr, tabs)
+    torch.cuda.synchronize(device)
+    ref = torch.from_numpy(np.stack(imgs)).to(device)
+    bad = [i for i in range(n) if not torch.equal(out[i, :, : fr.width], ref[i])]
+    assert not bad, (kind, bad[:8])
+
+
 @pytest.mark.parametrize("prepared", [True, False])
 @pytest.mark.parametrize("flags", [0, 1])
 def test_zero_width_windows_match_reference(mh, oracle, device, prepared, flags):
