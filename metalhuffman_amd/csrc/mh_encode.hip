@@ -177,14 +177,16 @@ __device__ __forceinline__ uint64_t row_symbols(uint64_t q, uint32_t r, bool del
 constexpr uint32_t kTileGroups = kCodeTile / 32;
 static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgroup's batch covers a code tile");
 // Blocks per tile of the batched path (split workgroup, tree tile counts, packer wave).
-// Bigger tiles halve the per-tile records (counts, offsets, last-block symbols) the
-// split writes and the trees read; A/B builds set MH_BATCH_TILE.
+// 256 (round 5) halves round 4's per-tile records (counts, offsets, last-block symbols)
+// that the split writes and the trees read: 64 BigBridge shuffles per call, 571 -> 557 MB
+// of HBM traffic and 3.02-3.07 -> 2.88-2.93 us per frame (profiles/r05_encoder_batch_ab.txt).
+// A/B builds set MH_BATCH_TILE.
 #ifndef MH_BATCH_TILE
-#define MH_BATCH_TILE 128
+#define MH_BATCH_TILE 256
 #endif
 constexpr uint32_t kBatchTile = MH_BATCH_TILE;
-static_assert(kBatchTile / 32 <= kSplitBatch && kBatchTile % 32 == 0 && kBatchTile * 64 < 65536,
-              "a split workgroup's batch covers a batch tile; u16 tile counts");
+static_assert(kBatchTile / 32 <= 2 * kSplitBatch && kBatchTile % 32 == 0 && kBatchTile * 64 < 65536,
+              "a split workgroup loads a batch tile's rows at once; u16 tile counts");
 
 // Row r of this lane's block (32 g + lane / 8) of group g as ONE unconditional buffer
 // load (kVec: 8 bytes; else 8 byte loads), zero past the frame: a fixed count of loads
