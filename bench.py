@@ -16,8 +16,12 @@ Every clocked region is COLD, as every frame of the reference's renderer is new 
 K eager launches of a region take the next K resident frames; the long launches --
 the 64-frame batch, the 8192^2 frame -- cycle over >= 2 launches of >= 337 MB), and
 a 1 GiB device copy evicts the 256 MiB Infinity Cache and the L2s right before the
-region, off the clock. The previous rounds' warm method (the clocked region
-re-decodes the frames the region before it decoded) is reported as `warm_value`.
+region, off the clock. `warm_value` is a region that re-decodes the launches the region
+before it decoded, without the flush: for the one-frame workload (20 frames, 106 MB)
+those inputs are still in the Infinity Cache; for the long launches, which cycle over
+>= 2 launch sets of >= 113 MB, they are not, so there warm ~ cold. Round 3's method (one
+resident launch re-decoded: the 138 MB random frame entirely in the 256 MiB cache) runs
+the same kernels 5-11 % faster (profiles/r05_bisect_ab.txt).
 The K launches are enqueued behind a launch gate before the clock starts (short
 launches eagerly, long ones as hipGraph replays). `roofline.kernel_us_avg` is the
 timed region's own steady launch period from HIP events on the launch stream.
@@ -361,7 +365,7 @@ class Workload:
 
         if GATE.ok():
             timed(events=False, cold=False)  # the gate's own first launch off the clock
-            # warm (the previous rounds' method, reported beside): the same launches again
+            # warm (reported beside): the same launches again, no flush
             self.warm_wall, _, _ = timed(events=False, cold=False)
             # The clocked region holds only the K launches: its two HIP event records
             # (markers in the queue) cost ~7 us per region at 20 steps (510 vs 482 x10^3
@@ -999,8 +1003,9 @@ def main(argv=None) -> int:
                    "the timed region" if wl.ungated_wall is not None else "plain"),
     }
     if wl.warm_wall is not None:
-        # the previous rounds' method: the clocked region re-decodes the launches the
-        # region before it just decoded (inputs warm in the Infinity Cache)
+        # the clocked region re-decodes the launches the region before it just decoded,
+        # no flush (still cache-resident for one-frame launches; not for the long
+        # launches, whose launch sets cycle: see the docstring)
         result["warm_ms_per_step"] = round(wl.warm_wall / args.steps * 1e3, 5)
         result["warm_value"] = round(world * wl.pixels / (wl.warm_wall / args.steps) / 1e6, 1)
     if wl.ungated_wall is not None:
