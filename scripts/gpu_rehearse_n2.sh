@@ -13,4 +13,5 @@ import json
 d = json.loads(open('gpurun_out/bench_n2_gloo.json').read().strip().splitlines()[-1])
 print('n_gpus', d['n_gpus'], 'value', d['value'], 'ms_per_step', d['ms_per_step'], d['config'].get('launch'))
 print('extras', sorted(d.get('extras', {}).keys()))
+print('ranks_verified', d.get('ranks_verified'), 'rank_devices', d.get('rank_devices'))
 "
