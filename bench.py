@@ -110,7 +110,9 @@ FLUSH_BYTES = 512 << 20  # x2 buffers: 1 GiB of HBM traffic, 4x the 256 MiB Infi
 class _Flush:
     """Evicts the Infinity Cache (MALL, 256 MiB) and the XCD L2s before a cold timed
     region: one device copy of 512 MiB (512 MiB read + 512 MiB written), issued on the
-    launch stream before the region's opening synchronize, so it is off the clock."""
+    launch stream before the region's opening synchronize, so it is off the clock. (A
+    read-only eviction -- a reduction over 1 GiB, nothing left dirty -- left the batch
+    and 8192^2 launches 7-10 % slower: profiles/r05_flush_method_ab.txt.)"""
 
     def __init__(self):
         self.bufs = {}
