@@ -311,53 +311,67 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
   const uint32_t r = threadIdx.x & 7u;
   const uint32_t copy = threadIdx.x % kHistCopies;
   const bool delta = !(flags & MH_FLAG_NO_DELTA);
-  // block_init: buffer stores (a fixed count, lanes without a byte out of range)
+  // block_init: buffer stores (lanes without a byte out of range)
   const __amdgpu_buffer_rsrc_t rinit = enc_rsrc(block_init, block_init ? nb : 0ull);
   // one group of 32 blocks: deltas, init bytes, symbols out (four-kernel path; the
   // fused path's packer re-derives them from the pixels), histogram
+  // one group of 32 blocks (four-kernel path): deltas, init bytes, symbols out, histogram
   auto process = [&](uint64_t g, uint64_t q) {
     const uint64_t b = g * 32 + (threadIdx.x >> 3);
-    const bool on = kTiled ? (uint32_t)b < (uint32_t)nb : b < nb;  // tiled: one frame, < 2^26 blocks
+    const bool on = b < nb;
     uint32_t first;
     const uint64_t v = row_symbols(q, r, delta, block_init != nullptr, &first);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && on ? (uint32_t)b : kOob), 0, 0);
     if (on) {
-      if constexpr (!kTiled) {  // the four-kernel path's symbol buffer (large frames: 64-bit offsets)
-        if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;
-      }
+      if (sym) reinterpret_cast<uint64_t *>(sym + b * 64)[r] = v;  // large frames: 64-bit offsets
       for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
-      // batched path: the tile's last block's symbols, for the next tile's packer (its
-      // first code word starts with this block's last bits); 64 B per tile instead of
-      // the packer re-reading the block's eight pixel rows (eight 128-B lines) from HBM
-      if (tiled && tile_tail && (uint32_t)b == wg * kTile + (kTile - 1u)) tile_tail[(uint64_t)wg * 8u + r] = v;
     }
   };
-  // kSplitBatch groups' rows are loaded before any is processed: 8 bytes per lane in
-  // flight would leave the frame's read latency-bound
   const uint64_t ngroups = (nb + 31) / 32;
-  // grid-stride over groups, or (tiled) one batch of consecutive groups
-  const uint64_t ustep = tiled ? 1u : gridDim.x;
   constexpr uint32_t kGroups = kTile / 32;  // tiled: groups of 32 blocks per tile
-  const uint64_t gfirst = tiled ? (uint64_t)wg * kGroups : blockIdx.x;
-  const uint64_t gstride = tiled ? ngroups : (uint64_t)kSplitBatch * gridDim.x;
-  for (uint64_t g0 = gfirst; g0 < ngroups; g0 += gstride) {
-    constexpr uint32_t nu = kTiled ? kGroups : kSplitBatch;
-    uint64_t q[nu];
-    if constexpr (kTiled) {
-      tile_rows<kVec, nu, kTile>(gray, W, H, bw, nb, (uint32_t)g0 * 32u, r, q);
-    } else {
-#pragma unroll
-      for (uint32_t u = 0; u < nu; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * ustep, r);
-    }
-    if (!cleared) clear_hist();  // workgroup-uniform
+  if constexpr (kTiled) {
+    // One tile: its kGroups groups' rows loaded at once (8 bytes per lane in flight would
+    // leave the read latency-bound), then each group's deltas and histogram. The init
+    // bytes are stored only when the format has them (a uniform branch: no dead store per
+    // row), and the tile's last block's symbols (batched path, tile_tail) once at the end.
+    const uint32_t nb32 = (uint32_t)nb, tb = wg * kTile;
+    uint64_t q[kGroups];
+    tile_rows<kVec, kGroups, kTile>(gray, W, H, bw, nb, tb, r, q);
+    clear_hist();
 #if MH_CODE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     MH_SPLIT_STAMP(1)
 #endif
+    uint64_t vlast = 0;
 #pragma unroll
-    for (uint32_t u = 0; u < nu; ++u) {
-      const uint64_t g = g0 + u * ustep;
-      if (g < ngroups) process(g, q[u]);
+    for (uint32_t u = 0; u < kGroups; ++u) {
+      const uint32_t b = tb + 32u * u + (threadIdx.x >> 3);
+      uint32_t first;
+      const uint64_t v = row_symbols(q[u], r, delta, block_init != nullptr, &first);
+      if (block_init)  // kernel-uniform
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && b < nb32 ? b : kOob), 0, 0);
+      if (b < nb32)
+        for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
+      vlast = v;
+    }
+    // the tile's last block (lanes 248-255 of group kGroups - 1): its symbols for the next
+    // tile's packer, whose first code word starts with this block's last bits -- 64 B per
+    // tile instead of the packer re-reading the block's eight pixel rows (eight 128-B lines)
+    if (tile_tail && threadIdx.x >= 248u && tb + kTile - 1u < nb32) tile_tail[(uint64_t)wg * 8u + r] = vlast;
+  } else {
+    // grid-stride over groups, kSplitBatch groups' rows loaded before any is processed
+    // (32-bit group indices: a frame has < 2^26 blocks, < 2^21 groups)
+    const uint32_t ng32 = (uint32_t)ngroups, gdim = gridDim.x, gstride = kSplitBatch * gdim;
+    for (uint32_t g0 = blockIdx.x; g0 < ng32; g0 += gstride) {
+      uint64_t q[kSplitBatch];
+#pragma unroll
+      for (uint32_t u = 0; u < kSplitBatch; ++u) q[u] = group_row<kVec>(gray, W, H, bw, nb, g0 + u * gdim, r);
+      if (!cleared) clear_hist();  // workgroup-uniform
+#pragma unroll
+      for (uint32_t u = 0; u < kSplitBatch; ++u) {
+        const uint32_t g = g0 + u * gdim;
+        if (g < ng32) process(g, q[u]);
+      }
     }
   }
   MH_SPLIT_STAMP(2)
