@@ -1379,7 +1379,10 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
   // gathers need no per-wave base: one VALU per symbol for the address)
   __shared__ uint32_t tab[256];
   __shared__ __attribute__((aligned(16))) uint32_t s_w[kPackWaves][kStepSlots];
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, k = lane >> 3, r = lane & 7u;
+  // the wave index as a provably uniform value (readfirstlane): the tile, its offsets and
+  // the step cursor then live in SGPRs (SALU) instead of being carried per lane
+  const uint32_t lane = threadIdx.x & 63u, k = lane >> 3, r = lane & 7u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t f = blockIdx.x / ncode_wg, t = (blockIdx.x - f * ncode_wg) * kPackWaves + wave;
   if (!(uint32_t)meta[(uint64_t)f * kMetaWords + 1]) return;  // rejected frame (workgroup-uniform): nothing written
   {
