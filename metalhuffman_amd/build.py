@@ -23,8 +23,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MH_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = {
+    # kernarg preload: the decode kernels' leading scalar arguments arrive in SGPRs at wave
+    # launch, so their first loads need no scalar load of the kernarg segment
     "mh_decode.o": ("mh_decode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-                                      "-Wall", "-c"]),
+                                      "-Wall", "-mllvm", "-amdgpu-kernarg-preload-count=16", "-c"]),
     "mh_tables.o": ("mh_tables.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                                       "-Wall", "-c"]),
     "mh_encode.o": ("mh_encode.hip", [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",

@@ -677,7 +677,21 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 // -> escape-free; one code length only -> escape-free with the swizzled stage. An
 // in-kernel table (no prepared LUT) keeps the general step.
 template <bool kDelta>
-__global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(const DecodeArgs a) {
+// Leading scalar arguments: preloaded into SGPRs at wave launch (as the small kernel's).
+__global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode_kernel(
+    const uint32_t *p_offsets, const uint64_t *p_frame_off, const uint8_t *p_block_init, const uint16_t *p_lut,
+    uint32_t p_nb, uint32_t p_tiles_per_frame, uint32_t p_total_tiles, uint32_t p_nwaves, uint32_t p_grid,
+    const DecodeArgs a0) {
+  DecodeArgs a = a0;
+  a.offsets = p_offsets;
+  a.frame_off = p_frame_off;
+  a.block_init = p_block_init;
+  a.lut = p_lut;
+  a.nb = p_nb;
+  a.tiles_per_frame = p_tiles_per_frame;
+  a.total_tiles = p_total_tiles;
+  a.nwaves = p_nwaves;
+  a.grid = p_grid;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = a.nwaves;
@@ -768,7 +782,21 @@ __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  //
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
 
 template <bool kDelta>
-__global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(const DecodeArgs a) {
+// The kernel arguments the first loads depend on come first, as scalars: the code object
+// preloads the leading kernarg dwords into SGPRs at wave launch (amdgpu-kernarg-preload,
+// build.py), so the block-offset and table loads issue without waiting for a scalar load
+// of the kernarg segment; the rest of DecodeArgs is read from memory behind them.
+__global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
+    const uint32_t *p_offsets, const uint64_t *p_frame_off, const uint8_t *p_block_init, const uint16_t *p_lut,
+    uint32_t p_nb, uint32_t p_tiles_per_frame, uint32_t p_total_tiles, const DecodeArgs a0) {
+  DecodeArgs a = a0;
+  a.offsets = p_offsets;
+  a.frame_off = p_frame_off;
+  a.block_init = p_block_init;
+  a.lut = p_lut;
+  a.nb = p_nb;
+  a.tiles_per_frame = p_tiles_per_frame;
+  a.total_tiles = p_total_tiles;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr uint32_t nwaves = kSmallWaves;  // launched with kSmallWaves waves per workgroup
@@ -1219,12 +1247,12 @@ const DeviceInfo *device_info(hipStream_t s) {
 
 // One kernel launch; any_order (MH_FLAG_ANY_ORDER) clears the dispatch packet's
 // barrier bit so the kernel may start while earlier work on the stream drains.
-#define MH_LAUNCH(kernel, grid, block, s, any_order, arg)                                          \
+#define MH_LAUNCH(kernel, grid, block, s, any_order, ...)                                          \
   do {                                                                                            \
     if (any_order)                                                                                \
-      hipExtLaunchKernelGGL(kernel, grid, block, 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, arg); \
+      hipExtLaunchKernelGGL(kernel, grid, block, 0, s, nullptr, nullptr, hipExtAnyOrderLaunch, __VA_ARGS__); \
     else                                                                                          \
-      hipLaunchKernelGGL(kernel, grid, block, 0, s, arg);                                         \
+      hipLaunchKernelGGL(kernel, grid, block, 0, s, __VA_ARGS__);                                 \
   } while (0)
 
 template <bool kDelta>
@@ -1251,7 +1279,8 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
     // table (measured: 8-wave groups beat one 3-wave group per CU by ~5 %)
     const uint32_t nw = kSmallWaves;
     a.n_groups = (a.total_tiles + nw - 1) / nw;
-    MH_LAUNCH(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), s, any_order, a);
+    MH_LAUNCH(mh_decode_small_kernel<kDelta>, dim3(a.n_groups), dim3(nw * 64), s, any_order, a.offsets,
+              a.frame_off, a.block_init, a.lut, a.nb, a.tiles_per_frame, a.total_tiles, a);
     return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
   }
   // Waves per workgroup: spread a small launch (one 2048x1536 frame = 768 tiles)
@@ -1264,7 +1293,8 @@ int launch(const DecodeArgs &a0, hipStream_t s, bool lane_pairs, bool any_order)
   const uint32_t grid = a.n_groups < resident ? a.n_groups : resident;
   a.nwaves = nw;
   a.grid = grid;
-  MH_LAUNCH(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), s, any_order, a);
+  MH_LAUNCH(mh_decode_kernel<kDelta>, dim3(grid), dim3(nw * 64), s, any_order, a.offsets, a.frame_off,
+            a.block_init, a.lut, a.nb, a.tiles_per_frame, a.total_tiles, a.nwaves, a.grid, a);
   return hipGetLastError() == hipSuccess ? MH_OK : MH_ERR_HIP;
 }
 
