@@ -776,7 +776,10 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 // single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
-constexpr int kSmallWaves = 4;  // waves per workgroup (one tile each)
+#ifndef MH_SMALL_WAVES          // A/B builds only
+#define MH_SMALL_WAVES 4
+#endif
+constexpr int kSmallWaves = MH_SMALL_WAVES;  // waves per workgroup (one tile each)
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
