@@ -46,7 +46,10 @@ constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = wh
 // Small-launch kernel: nt sc1, write-through, so nothing dirty is left in the XCDs'
 // L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt).
 constexpr int kBatchStoreAux = 2;
-constexpr int kSmallStoreAux = 18;
+#ifndef MH_SMALL_STORE_AUX      // A/B builds only
+#define MH_SMALL_STORE_AUX 18
+#endif
+constexpr int kSmallStoreAux = MH_SMALL_STORE_AUX;
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
