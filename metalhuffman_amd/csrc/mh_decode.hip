@@ -45,7 +45,10 @@ constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = wh
 // Row-store cache bits (gfx950 aux field: 1 sc0, 2 nt, 16 sc1). Batch kernel: nt.
 // Small-launch kernel: nt sc1, write-through, so nothing dirty is left in the XCDs'
 // L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt).
-constexpr int kBatchStoreAux = 2;
+#ifndef MH_BATCH_STORE_AUX      // A/B builds only
+#define MH_BATCH_STORE_AUX 2
+#endif
+constexpr int kBatchStoreAux = MH_BATCH_STORE_AUX;
 #ifndef MH_SMALL_STORE_AUX      // A/B builds only
 #define MH_SMALL_STORE_AUX 18
 #endif
