@@ -49,12 +49,6 @@ constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = wh
 #define MH_BATCH_STORE_AUX 2
 #endif
 constexpr int kBatchStoreAux = MH_BATCH_STORE_AUX;
-#ifndef MH_SMALL_DEFER_STORES   // A/B builds only: the small kernel's row stores after the block
-#define MH_SMALL_DEFER_STORES 0
-#endif
-#ifndef MH_SMALL_ROLLED         // A/B builds only: the small kernel's 8-row loop not unrolled
-#define MH_SMALL_ROLLED 0
-#endif
 #ifndef MH_SMALL_STORE_AUX      // A/B builds only
 #define MH_SMALL_STORE_AUX 18
 #endif
@@ -207,11 +201,9 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 // kMasked: only the lanes that consumed a word read the next one (batch kernel);
 //   the small-launch kernel's latency-bound chain reads unmasked.
 template <int kBits, bool kMaskedRefill, bool kEscapes = kBits == kLutBits, bool kSwizzle = false,
-          int kStoreAux = kBatchStoreAux, bool kRolledRows = false, bool kDeferStores = false>
+          int kStoreAux = kBatchStoreAux>
 struct StepCfg {
   static constexpr int kAux = kStoreAux;  // row-store cache bits
-  static constexpr bool kRolled = kRolledRows;  // the 8-row loop not unrolled (smaller code)
-  static constexpr bool kDefer = kDeferStores;  // the 8 row stores after the block, not per row
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
   static constexpr bool kMasked = kMaskedRefill;
@@ -326,61 +318,36 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   // dead lanes store at >= 2^31 + r * pitch: past every output descriptor's range
   // (<= 0x7FFFFFF0 bytes), so the hardware drops them -- one select per tile, not per row
   const uint32_t rbase = dead ? 0x80000000u : row0;
-  // Each finished row is one unconditional 8-byte store (exact vmcnt counting): lanes
-  // without a block and rows below the frame use offsets outside the descriptor's
-  // range, which the hardware drops. A right-edge block writes its 8 bytes into the
-  // row's pitch padding (pitch >= round_up(W, 8)).
-#define MH_ROW_BODY(r)                                                               \
-    uint32_t o0 = 0, o1 = 0;                                                         \
-    uint32_t sv[4];  /* S after each symbol of the current output word (delta) */    \
-    (void)sv;                                                                        \
-    if (r) {                                                                         \
-      MH_STEP_R(0, o0);                                                              \
-    } else {                                                                         \
-      MH_STEP(0, o0);                                                                \
-    }                                                                                \
-    MH_STEP(1, o0);                                                                  \
-    MH_STEP_R(2, o0);                                                                \
-    MH_STEP(3, o0);                                                                  \
-    if (kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);                         \
-    MH_STEP_R(0, o1);                                                                \
-    MH_STEP(1, o1);                                                                  \
-    MH_STEP_R(2, o1);                                                                \
-    MH_STEP(3, o1);                                                                  \
-    if (kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);                         \
-    if constexpr (Cfg::kDefer) {                                                     \
-      rows[r][0] = o0;                                                               \
-      rows[r][1] = o1;                                                               \
-    } else {                                                                         \
-      typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));                \
-      v2u32 v;                                                                       \
-      v.x = o0;                                                                      \
-      v.y = o1;                                                                      \
-      const uint32_t off = rbase + r * pitch;                                        \
-      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, Cfg::kAux);         \
-    }
-  uint32_t rows[8][2];
-  (void)rows;
-  if constexpr (Cfg::kRolled) {
-#pragma unroll 1
-    for (uint32_t r = 0; r < 8; ++r) {
-      MH_ROW_BODY(r)
-    }
-  } else {
 #pragma unroll
-    for (uint32_t r = 0; r < 8; ++r) {
-      MH_ROW_BODY(r)
+  for (uint32_t r = 0; r < 8; ++r) {
+    uint32_t o0 = 0, o1 = 0;
+    uint32_t sv[4];  // S after each symbol of the current output word (delta mode)
+    (void)sv;
+    if (r) {
+      MH_STEP_R(0, o0);
+    } else {
+      MH_STEP(0, o0);
     }
-  }
-#undef MH_ROW_BODY
-  if constexpr (Cfg::kDefer) {
-#pragma unroll
-    for (uint32_t r = 0; r < 8; ++r) {
+    MH_STEP(1, o0);
+    MH_STEP_R(2, o0);
+    MH_STEP(3, o0);
+    if (kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    MH_STEP_R(0, o1);
+    MH_STEP(1, o1);
+    MH_STEP_R(2, o1);
+    MH_STEP(3, o1);
+    if (kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
+    // block and rows below the frame use offsets outside the descriptor's range,
+    // which the hardware drops. A right-edge block writes its 8 bytes into the
+    // row's pitch padding (pitch >= round_up(W, 8)).
+    {
       typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
       v2u32 v;
-      v.x = rows[r][0];
-      v.y = rows[r][1];
-      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)(rbase + r * pitch), 0, Cfg::kAux);
+      v.x = o0;
+      v.y = o1;
+      const uint32_t off = rbase + r * pitch;
+      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)off, 0, Cfg::kAux);
     }
   }
 #undef MH_STEP
@@ -889,10 +856,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
   const uint32_t row0 = ot.row0;
   // the small kernel's step flavours (all with write-through row stores)
-  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux, MH_SMALL_ROLLED != 0,
-                          MH_SMALL_DEFER_STORES != 0>;
-  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux, MH_SMALL_ROLLED != 0,
-                          MH_SMALL_DEFER_STORES != 0>;
+  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux>;
+  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux>;
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
