@@ -36,6 +36,12 @@ namespace {
 #ifndef MH_DIAG_STAMPS          // diagnostic builds only: per-wave phase timestamps
 #define MH_DIAG_STAMPS 0        //    (scripts/diag_stamps.py)
 #endif
+#ifndef MH_DIAG_CLOCK           // diagnostic builds only: core-clock cycles of the single-frame
+#define MH_DIAG_CLOCK 0         //    decode in stamp slot 5 (scripts/diag_stamps.py --clock)
+#endif
+#ifndef MH_DIAG_DROP_STORES     // diagnostic builds only: every row store out of range (dropped)
+#define MH_DIAG_DROP_STORES 0
+#endif
 #ifndef MH_LANE_PAIRS           // 1: the lane-pair diagnostic library only (libmh_diag_lanepairs.so,
 #define MH_LANE_PAIRS 0         //    metalhuffman_amd/build.py), which exports mh_diag_decode_lanepairs
 #endif
@@ -317,7 +323,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
 
   // dead lanes store at >= 2^31 + r * pitch: past every output descriptor's range
   // (<= 0x7FFFFFF0 bytes), so the hardware drops them -- one select per tile, not per row
-  const uint32_t rbase = dead ? 0x80000000u : row0;
+  const uint32_t rbase = (dead || MH_DIAG_DROP_STORES) ? 0x80000000u : row0;
 #pragma unroll
   for (uint32_t r = 0; r < 8; ++r) {
     uint32_t o0 = 0, o1 = 0;
@@ -782,6 +788,9 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 // single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
+#ifndef MH_SMALL_TOUCH          // A/B builds only: 1 = at entry, touch the tile's output rows
+#define MH_SMALL_TOUCH 0        //    and the frame's codes near the tile's linear share (TLB warm-up)
+#endif
 #ifndef MH_SMALL_WAVES          // A/B builds only
 #define MH_SMALL_WAVES 4
 #endif
@@ -836,6 +845,24 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
     for (int k = 0; k < kLutLoads; ++k)
       L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + 64u * kSmallWaves * k) * 16u), 0, 0);
   }
+#if MH_SMALL_TOUCH
+  // one-frame launches: translate the pages the later, dependent accesses use while the
+  // offsets' round trip is in flight (lanes 0/1: the tile's first / last output row; lane 2:
+  // the codes byte at the tile's linear share of the frame)
+  uint32_t touch = 0;
+  if (a.total_tiles <= a.tiles_per_frame && tile < a.total_tiles) {
+    const uint32_t by0 = (tile * 64u) / a.bw;
+    const uint64_t base = (uint64_t)by0 * 8u * a.out_pitch;
+    const uint64_t rem = a.out_frame_bytes > base ? a.out_frame_bytes - base : 0u;
+    const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(a.out + base, (uint32_t)(rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull));
+    const uint32_t oo = lane < 2u ? lane * 7u * (uint32_t)a.out_pitch : 0xFFFFFFF0u;
+    touch = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)oo, 0, 0);
+    const uint32_t cb = a.codes_bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)a.codes_bytes;
+    const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(a.codes, cb);
+    const uint32_t co = lane == 2u ? (uint32_t)(((uint64_t)cb * tile) / a.total_tiles) & ~3u : 0xFFFFFFF0u;
+    touch += __builtin_amdgcn_raw_buffer_load_b32(rc, (int)co, 0, 0);
+  }
+#endif
   const Tile t = hdr_resolve(a, h, lane);
   MH_STAMP(1);
   const bool live = t.tile < a.total_tiles;
@@ -858,10 +885,16 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   // the small kernel's step flavours (all with write-through row stores)
   using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux>;
   using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux>;
+#if MH_DIAG_STAMPS && MH_DIAG_CLOCK
+  unsigned long long c3 = 0;
+#endif
   if (staged) {
     span_write(t, lane, R, stage);
     wave_sync();
     MH_STAMP(3);
+#if MH_DIAG_STAMPS && MH_DIAG_CLOCK
+    c3 = __builtin_amdgcn_s_memtime();
+#endif
     LdsWords src{stage};
     if (l14)
       decode_block<kDelta, Small14>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
@@ -872,9 +905,16 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   } else {
     decode_halves<kDelta, Small13>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
+#if MH_SMALL_TOUCH
+  asm volatile("" ::"v"(touch));
+#endif
 #if MH_DIAG_STAMPS
   MH_STAMP(4);
+#if MH_DIAG_CLOCK
+  ts[5] = staged ? __builtin_amdgcn_s_memtime() - c3 : 0ull;  // core clocks of the decode
+#else
   ts[5] = ts[4];
+#endif
   __builtin_amdgcn_s_waitcnt(0);
   MH_STAMP(6);
   const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]

@@ -24,6 +24,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--tag", default="")
+ap.add_argument("--clock", action="store_true",
+                help="MH_DIAG_CLOCK build: slot 5 holds the decode's core-clock cycles (s_memtime)")
 ap.add_argument("--tile8192", action="store_true", help="config 3: one 8192x8192 BigBridge mirror tile")
 ap.add_argument("--cold", action="store_true",
                 help="stamp a launch of a second, never-decoded frame set after a 1 GiB cache flush (bench.py's cold rule)")
@@ -66,6 +68,15 @@ live = st[:, 0] > 0
 st = st[live]
 t0 = st[:, 0].min()
 print(f"launch event time {s0.elapsed_time(s1) * 1e3:.2f} us; waves {live.sum()}")
+if args.clock:  # slot 5 = s_memtime cycles between stamps 3 and 4 (staged tiles only)
+    cyc = st[:, 5].astype(np.int64)
+    us = (st[:, 4].astype(np.int64) - st[:, 3].astype(np.int64)) * 0.01
+    ok = (cyc > 0) & (us > 0)
+    mhz = cyc[ok] / us[ok]
+    print(f"decode core cycles p50 {np.median(cyc[ok]):.0f} p90 {np.percentile(cyc[ok], 90):.0f}; "
+          f"per symbol p50 {np.median(cyc[ok]) / 64:.1f}; clock MHz p10 {np.percentile(mhz, 10):.0f} "
+          f"p50 {np.median(mhz):.0f} p90 {np.percentile(mhz, 90):.0f}")
+    st[:, 5] = st[:, 4]
 names = ["entry", "hdr", "lut", "staged", "tile0", "loop", "drain"]
 for i, nm in enumerate(names):
     v = (st[:, i].astype(np.int64) - int(t0)) * 0.01
