@@ -206,9 +206,14 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 //          longer than 14 bits (the prepared table records the longest code).
 // kMasked: only the lanes that consumed a word read the next one (batch kernel);
 //   the small-launch kernel's latency-bound chain reads unmasked.
+// kLazy: the refill test runs at every step on the cursor the lookup itself uses, in the
+//   lookup's LDS shadow, and takes effect at the next step (sh <= 47 still holds at every
+//   lookup: sh >= 32 drops a word, sh < 32 advances by <= 16), so the chain from one
+//   lookup to the next is add, shift, and -- no compare / select on it.
 template <int kBits, bool kMaskedRefill, bool kEscapes = kBits == kLutBits, bool kSwizzle = false,
-          int kStoreAux = kBatchStoreAux>
+          int kStoreAux = kBatchStoreAux, bool kLazyRefill = false>
 struct StepCfg {
+  static constexpr bool kLazy = kLazyRefill;
   static constexpr int kAux = kStoreAux;  // row-store cache bits
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
@@ -309,6 +314,23 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     S += d * 8u;                                                                    \
     if constexpr (!Cfg::kMasked) nw = rd(wa + 8);                                   \
   }
+#define MH_STEP_L(J, OW)                                                            \
+  {                                                                                 \
+    const uint64_t x = (((uint64_t)hi) << 32) | lo;                                 \
+    MH_LOOKUP((uint32_t)(x >> (S & 63u)) & Cfg::kMask)                              \
+    /* off the chain: refill from the cursor this lookup used */                    \
+    const bool c = (S & 0xFFu) <= kRefill;                                         \
+    hi = c ? lo : hi;                                                               \
+    lo = c ? nw : lo;                                                               \
+    const uint32_t d = c ? 4u : 0u;                                                 \
+    wa += d;                                                                        \
+    S += d * 8u;                                                                    \
+    /* keep S + d*8 one add ahead of S + e (else it is re-associated onto the  */  \
+    /* chain), and the selects as selects                                       */  \
+    asm volatile("" : "+v"(S), "+v"(hi), "+v"(lo));                                \
+    nw = rd(wa + 8);                                                                \
+    MH_FINISH(J, OW)                                                                \
+  }
 #define MH_STEP_R(J, OW)                                                            \
   {                                                                                 \
     const bool c = (S & 0xFFu) <= kRefill;                                         \
@@ -329,6 +351,18 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     uint32_t o0 = 0, o1 = 0;
     uint32_t sv[4];  // S after each symbol of the current output word (delta mode)
     (void)sv;
+    if constexpr (Cfg::kLazy) {
+      MH_STEP_L(0, o0);
+      MH_STEP_L(1, o0);
+      MH_STEP_L(2, o0);
+      MH_STEP_L(3, o0);
+      if (kDelta) o0 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+      MH_STEP_L(0, o1);
+      MH_STEP_L(1, o1);
+      MH_STEP_L(2, o1);
+      MH_STEP_L(3, o1);
+      if (kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    } else {
     if (r) {
       MH_STEP_R(0, o0);
     } else {
@@ -343,6 +377,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     MH_STEP_R(2, o1);
     MH_STEP(3, o1);
     if (kDelta) o1 = pack_prev4(sv[0], sv[1], sv[2], sv[3]);
+    }
     // Unconditional 8-byte row store (exact vmcnt counting): lanes without a
     // block and rows below the frame use offsets outside the descriptor's range,
     // which the hardware drops. A right-edge block writes its 8 bytes into the
@@ -358,6 +393,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   }
 #undef MH_STEP
 #undef MH_STEP_R
+#undef MH_STEP_L
 #undef MH_LOOKUP
 #undef MH_FINISH
 #undef MH_REFILL_C
@@ -791,6 +827,9 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 #ifndef MH_SMALL_TOUCH          // A/B builds only: 1 = at entry, touch the tile's output rows
 #define MH_SMALL_TOUCH 0        //    and the frame's codes near the tile's linear share (TLB warm-up)
 #endif
+#ifndef MH_SMALL_LAZY           // A/B builds only: 1 = lazy refill in the small kernel's steps
+#define MH_SMALL_LAZY 0
+#endif
 #ifndef MH_SMALL_WAVES          // A/B builds only
 #define MH_SMALL_WAVES 4
 #endif
@@ -883,8 +922,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
   const uint32_t row0 = ot.row0;
   // the small kernel's step flavours (all with write-through row stores)
-  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux>;
-  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux>;
+  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux, MH_SMALL_LAZY>;
+  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux, MH_SMALL_LAZY>;
 #if MH_DIAG_STAMPS && MH_DIAG_CLOCK
   unsigned long long c3 = 0;
 #endif
