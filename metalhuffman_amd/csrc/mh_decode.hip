@@ -824,9 +824,6 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 // single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
-#ifndef MH_SMALL_TOUCH          // A/B builds only: 1 = at entry, touch the tile's output rows
-#define MH_SMALL_TOUCH 0        //    and the frame's codes near the tile's linear share (TLB warm-up);
-#endif                          //    2 = the codes touch only
 #ifndef MH_SMALL_LAZY           // 1: lazy refill in the small kernel's steps (0: A/B builds only;
 #define MH_SMALL_LAZY 1         //    profiles/r05_lazy_ab.txt)
 #endif
@@ -884,26 +881,6 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
     for (int k = 0; k < kLutLoads; ++k)
       L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + 64u * kSmallWaves * k) * 16u), 0, 0);
   }
-#if MH_SMALL_TOUCH
-  // one-frame launches: translate the pages the later, dependent accesses use while the
-  // offsets' round trip is in flight (lanes 0/1: the tile's first / last output row; lane 2:
-  // the codes byte at the tile's linear share of the frame)
-  uint32_t touch = 0;
-  if (a.total_tiles <= a.tiles_per_frame && tile < a.total_tiles) {
-#if MH_SMALL_TOUCH == 1
-    const uint32_t by0 = (tile * 64u) / a.bw;
-    const uint64_t base = (uint64_t)by0 * 8u * a.out_pitch;
-    const uint64_t rem = a.out_frame_bytes > base ? a.out_frame_bytes - base : 0u;
-    const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(a.out + base, (uint32_t)(rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull));
-    const uint32_t oo = lane < 2u ? lane * 7u * (uint32_t)a.out_pitch : 0xFFFFFFF0u;
-    touch = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)oo, 0, 0);
-#endif
-    const uint32_t cb = a.codes_bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)a.codes_bytes;
-    const __amdgpu_buffer_rsrc_t rc = uniform_rsrc(a.codes, cb);
-    const uint32_t co = lane == 2u ? (uint32_t)(((uint64_t)cb * tile) / a.total_tiles) & ~3u : 0xFFFFFFF0u;
-    touch += __builtin_amdgcn_raw_buffer_load_b32(rc, (int)co, 0, 0);
-  }
-#endif
   const Tile t = hdr_resolve(a, h, lane);
   MH_STAMP(1);
   const bool live = t.tile < a.total_tiles;
@@ -946,9 +923,6 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   } else {
     decode_halves<kDelta, Small13>(a, t, lane, lut, stage, out, row0, !t.valid);
   }
-#if MH_SMALL_TOUCH
-  asm volatile("" ::"v"(touch));
-#endif
 #if MH_DIAG_STAMPS
   MH_STAMP(4);
 #if MH_DIAG_CLOCK
