@@ -176,14 +176,7 @@ __device__ __forceinline__ constexpr uint32_t ins_sel1(int j) {
   return j == 0 ? 0x03020105u : j == 1 ? 0x03020500u : j == 2 ? 0x03050100u : 0x05020100u;
 }
 
-#ifndef MH_BATCH_L14            // A/B builds only: 1 = the batch kernel keeps a 32 KB table array and
-#define MH_BATCH_L14 0          //    decodes tables whose longest code is 14 bits with the single-level
-#endif                          //    14-bit table (no escape test; 2 workgroups per CU by LDS)
-#if MH_BATCH_L14
-__shared__ __attribute__((aligned(16))) uint16_t s_lut[kLut14Entries];
-#else
 __shared__ __attribute__((aligned(16))) uint16_t s_lut[kLutEntries];
-#endif
 __shared__ __attribute__((aligned(16))) uint8_t s_stage[kMaxWavesPerWG * kStageBytes];
 __shared__ uint32_t s_p0;
 
@@ -237,8 +230,6 @@ using Lut13NoEsc = StepCfg<kLutBits, true, false>;
 // ... and for flat tables (every code the same length, e.g. uniform bytes: every
 // block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
 using Lut13Flat = StepCfg<kLutBits, true, false, true>;
-// ... and (MH_BATCH_L14 builds) the single-level 14-bit table for codes of <= 14 bits
-using Lut14Masked = StepCfg<kLut14Bits, true, false>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -773,27 +764,6 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   // first span could be staged (profiles/r04_v3_tile_start_ab.txt). A launch with a
   // prepared table has >= 5 waves per workgroup (smaller ones take the small-launch
   // kernel), so 4 loads per thread cover the table.
-#if MH_BATCH_L14
-  uint32_t mx = 16, mn = 0;
-  if (a.lut) {
-    const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
-    mx = ml[0];
-    mn = ml[1];
-  }
-  constexpr uint32_t kLutPer = 4;
-  const bool l14 = a.lut && mx == (uint32_t)kLut14Bits && nthreads * kLutPer >= (uint32_t)(kLut14Bytes / 16);
-  const uint32_t kLutChunks = l14 ? (uint32_t)(kLut14Bytes / 16) : (uint32_t)(kLutBytes / 16);
-  const bool fixed_copy = a.lut && nthreads * kLutPer >= kLutChunks;
-  hdr_issue(a, t0, lane, hc);
-  v4u32 L[kLutPer];
-  {
-    const __amdgpu_buffer_rsrc_t rl = uniform_rsrc(reinterpret_cast<const uint8_t *>(a.lut) + (l14 ? kLut14Off : 0),
-                                                   fixed_copy ? kLutChunks * 16u : 0u);
-#pragma unroll
-    for (uint32_t k = 0; k < kLutPer; ++k)
-      L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * nthreads) * 16u), 0, 0);
-  }
-#else
   constexpr uint32_t kLutChunks = kLutBytes / 16, kLutPer = 4;
   const bool fixed_copy = a.lut && nthreads * kLutPer >= kLutChunks;
   v4u32 L[kLutPer];
@@ -804,20 +774,17 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
       L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * nthreads) * 16u), 0, 0);
   }
   hdr_issue(a, t0, lane, hc);
-#endif
   // The step flavour, from the prepared table's code lengths (kernel-uniform): issued
   // behind the first header, so no dependent load sits in front of it.
   //   2: one code length (flat) -> escape-free step, swizzled stage
   //   1: no code over 13 bits   -> escape-free step
   //   0: general step (escapes), also for an in-kernel table
-#if !MH_BATCH_L14
   uint32_t mx = 16, mn = 0;
   if (a.lut) {
     const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
     mx = ml[0];
     mn = ml[1];
   }
-#endif
   if (fixed_copy) {
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
 #pragma unroll
@@ -832,11 +799,6 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 
   // the escape-free flavours need a prepared table, so a full fixed copy (>= 5 waves)
   const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
-#if MH_BATCH_L14
-  if (l14)
-    batch_loop<kDelta, Lut14Masked>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
-  else
-#endif
   if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
