@@ -69,3 +69,39 @@ def lane_pair_oversize_deltas(seed: int = 0) -> np.ndarray:
     rest = np.concatenate([rest, np.zeros(n - 2048 - rest.size, np.uint8)])
     r.shuffle(rest)
     return np.concatenate([head, rest])
+
+
+def refill_extreme_deltas(n_symbols: int, width: int, height: int, seed: int = 0) -> np.ndarray:
+    """Deltas with a Fibonacci histogram over `n_symbols` symbols (deepest code
+    n_symbols - 1 bits) rearranged so that many blocks hold a prefix of p short codes
+    (p = 0..32, every bit alignment of the cursor) followed by a run of the LONGEST codes:
+    the decoders' refill points then see the cursor at its deepest (sh up to 47 bits into
+    the 64-bit window). The histogram, hence the code lengths, is unchanged."""
+    nb = (width // 8) * (height // 8)
+    d = fibonacci_deltas(n_symbols, nb * 64, seed=seed)
+    vals, counts = np.unique(d, return_counts=True)
+    order = np.argsort(counts, kind="stable")          # rarest (longest code) first
+    rare = np.concatenate([np.full(counts[i], vals[i], np.uint8) for i in order])
+    common = int(vals[order[-1]])                      # the 1-bit code
+    out = np.empty(nb * 64, np.uint8)
+    r_i = 0
+    pool = []
+    for b in range(nb):
+        p = b % 33
+        blk = np.full(64, common, np.uint8)
+        take = min(64 - p, rare.size - r_i)
+        blk[p:p + take] = rare[r_i:r_i + take]
+        r_i += take
+        out[b * 64:(b + 1) * 64] = blk
+    # the histogram must match the Fibonacci one: the loop above used at most the rare
+    # symbols once each; top up / trim the common symbol so the multiset is d's
+    want = np.bincount(d, minlength=256)
+    have = np.bincount(out, minlength=256)
+    diff = want[common] - have[common]
+    if diff < 0:  # too many common symbols: put the unused rare ones back in their place
+        left = rare[r_i:]
+        idx = np.nonzero(out == common)[0][-left.size:] if left.size else np.array([], np.int64)
+        out[idx] = left
+        pool = left
+    assert np.array_equal(np.bincount(out, minlength=256), want), "histogram changed"
+    return out

@@ -8,7 +8,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from helpers import fibonacci_deltas, golden, image_from_block_deltas
+from helpers import fibonacci_deltas, golden, image_from_block_deltas, refill_extreme_deltas
 
 
 def _frames(mh, bigbridge):
@@ -23,6 +23,9 @@ def _frames(mh, bigbridge):
     yield "fib16", mh.encode_frame(img), img
     raw = fibonacci_deltas(15, 128 * 64, seed=2).reshape(64, 128)
     yield "no_delta", mh.encode_frame(raw, flags=mh.MH_FLAG_NO_DELTA), raw
+    # runs of the longest (16-bit) codes after 0..32 one-bit codes: every cursor alignment
+    ext = image_from_block_deltas(refill_extreme_deltas(17, 256, 256, seed=4), 256, 256)
+    yield "refill_extremes", mh.encode_frame(ext), ext
 
 
 def test_serial_decoders_match_oracle(mh, oracle, bigbridge):

@@ -10,7 +10,8 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from helpers import fibonacci_deltas, golden, image_from_block_deltas, long_span_deltas
+from helpers import (fibonacci_deltas, golden, image_from_block_deltas, long_span_deltas,
+                     refill_extreme_deltas)
 
 pytestmark = pytest.mark.gpu
 
@@ -246,6 +247,27 @@ def test_small_launch_multi_frame_variants(mh, oracle, device, bigbridge, mode):
     for i, (im, ef) in enumerate(zip(imgs, efs)):
         assert np.array_equal(out[i], im), i
         assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
+
+
+@pytest.mark.parametrize("n_sym", [15, 17])
+@pytest.mark.parametrize("delta", [True, False])
+def test_small_kernel_refill_extremes(mh, oracle, device, n_sym, delta):
+    """The single-frame kernel's lazy refill (refill test on the cursor a lookup used,
+    applied one step later) at its deepest cursor: blocks of p = 0..32 one-bit codes and
+    then runs of the longest codes (14 bits: the 14-bit table; 16 bits: the 13-bit table
+    with escapes), so lookups see every bit alignment up to 47 bits into the window.
+    512x512 = 64 tiles, one launch of the small kernel; bit-exact vs input and oracle."""
+    d = refill_extreme_deltas(n_sym, 512, 512, seed=n_sym)
+    if delta:
+        img = image_from_block_deltas(d, 512, 512)
+        ef = mh.encode_frame(img)
+    else:  # raw symbols: the raster whose block split is d itself
+        img = np.ascontiguousarray(d.reshape(64, 64, 8, 8).transpose(0, 2, 1, 3).reshape(512, 512))
+        ef = mh.encode_frame(img, flags=mh.MH_FLAG_NO_DELTA)
+    assert ef.canon.max() == n_sym - 1
+    out = _decode([ef], device)[0]
+    assert np.array_equal(out, img)
+    assert np.array_equal(out, _oracle_decode(oracle, ef))
 
 
 @pytest.mark.parametrize("h", [2048, 2056])
