@@ -718,6 +718,107 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
   }
 }
 
+// Flat 8-bit tables (every code 8 bits: all 256 symbols, canonical, so code c is symbol c
+// -- checked against the whole LDS table by the caller): a block's 64 codes are its 64
+// symbol bytes, MSB-first bytes in stream order. A lane decodes its block with byte
+// arithmetic -- no table lookup and no serial bit cursor: 17 dwords of codes, realigned
+// by v_alignbyte, one SDWA byte add per symbol for the delta sum, 3 VALU per output word.
+// The uniform-random 8192^2 stress frame is such a table.
+// A tile with a block that does not start on a byte (no reference producer writes one)
+// takes the general flat step.
+__device__ __forceinline__ uint32_t pack_lo4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0400u);  // [a.0, b.0, 0, 0]
+  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000C0Cu);  // [0, 0, c.0, d.0]
+  return lo | hi;
+}
+
+#ifndef MH_BATCH_FLAT8           // 0: A/B builds only (the general flat step for flat 8-bit tables too)
+#define MH_BATCH_FLAT8 1
+#endif
+struct Flat8Codes {
+  uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
+};
+
+__device__ __forceinline__ void flat8_issue(const DecodeArgs &a, const Tile &t, Flat8Codes &c) {
+  // unconditional loads (a fixed count, exact vmcnt); a lane without a block reads far
+  // past the frame (out of range: 0, no access)
+  const __amdgpu_buffer_rsrc_t rc = codes_rsrc(a, t);
+  const uint32_t byte = t.start + (t.p >> 3);  // the block's first code byte (frame relative)
+  const uint32_t base = t.valid ? (byte & ~3u) : 0xFFFFFF00u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(base + 16u * k), 0, 0);
+    c.w[4 * k] = v.x;
+    c.w[4 * k + 1] = v.y;
+    c.w[4 * k + 2] = v.z;
+    c.w[4 * k + 3] = v.w;
+  }
+  c.w[16] = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(base + 64u), 0, 0);
+}
+
+template <bool kDelta>
+__device__ __forceinline__ void flat8_block(const DecodeArgs &a, const Tile &t, uint32_t lane, const Flat8Codes &c) {
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+  const uint32_t sb = (t.start + (t.p >> 3)) & 3u;
+  const OutTile ot = out_tile(a, t, lane);
+  const uint32_t rbase = t.valid ? ot.row0 : 0x80000000u;
+  const uint32_t pitch = (uint32_t)a.out_pitch;
+  uint32_t s = t.init;  // running delta sum (byte 0)
+#pragma unroll
+  for (uint32_t r = 0; r < 8; ++r) {
+    // stream bytes 8r .. 8r + 7 (little-endian in each word: byte i = symbol 4j + i)
+    const uint32_t c0 = __builtin_amdgcn_alignbyte(c.w[2 * r + 1], c.w[2 * r], sb);
+    const uint32_t c1 = __builtin_amdgcn_alignbyte(c.w[2 * r + 2], c.w[2 * r + 1], sb);
+    v2u32 v;
+    if (kDelta) {
+      uint32_t sv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = s = s + ((c0 >> (8 * i)) & 0xFFu);
+      v.x = pack_lo4(sv[0], sv[1], sv[2], sv[3]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sv[i] = s = s + ((c1 >> (8 * i)) & 0xFFu);
+      v.y = pack_lo4(sv[0], sv[1], sv[2], sv[3]);
+    } else {
+      v.x = c0;
+      v.y = c1;
+    }
+    __builtin_amdgcn_raw_buffer_store_b64(v, ot.rsrc, (int)(rbase + r * pitch), 0, kBatchStoreAux);
+  }
+}
+
+// The batch kernel's loop for flat 8-bit tables: the same static tile schedule, software
+// pipelined like batch_loop -- while a tile decodes, the next tile's codes and the one
+// after's header are in flight, all issued before this tile's row stores, so no wait
+// below is for a store.
+template <bool kDelta>
+__device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, uint8_t *stage, const uint8_t *lut,
+                                           uint32_t t0, uint32_t gstride, const TileHdr &hc) {
+  TileHdr h;
+  Flat8Codes cc, cn;
+  Tile cur = hdr_resolve(a, hc, lane);
+  flat8_issue(a, cur, cc);
+  hdr_issue(a, next_tile(a, t0, gstride), lane, h);
+  while (cur.tile < a.total_tiles) {  // wave-uniform
+    // a block off the byte grid: this tile and the rest in the slow loop below
+    if (__builtin_expect(__ballot(cur.valid && ((cur.p & 7u) != 0u)) != 0, 0)) break;
+    const Tile nxt = hdr_resolve(a, h, lane);
+    flat8_issue(a, nxt, cn);
+    hdr_issue(a, next_tile(a, nxt.tile, gstride), lane, h);
+    flat8_block<kDelta>(a, cur, lane, cc);
+    cur = nxt;
+    cc = cn;
+  }
+  // Slow loop (no reference producer gets here): the general flat step, no prefetch.
+  for (uint32_t t = cur.tile; t < a.total_tiles; t = next_tile(a, t, gstride)) {
+    __builtin_amdgcn_s_waitcnt(0);
+    TileHdr hs;
+    hdr_issue(a, t, lane, hs);
+    const Tile tt = hdr_resolve(a, hs, lane);
+    const OutTile ot = out_tile(a, tt, lane);
+    decode_halves<kDelta, Lut13Flat>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+  }
+}
+
 // The batch kernel: persistent workgroups (wave w of workgroup g decodes tiles
 // g*W + w, + grid*W, ...). A common prologue (table copy, first two headers, first
 // span) and then one instantiation of the persistent loop per step flavour, chosen
@@ -799,7 +900,17 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 
   // the escape-free flavours need a prepared table, so a full fixed copy (>= 5 waves)
   const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
-  if (flavor == 1)
+  // flat 8-bit and canonical (code c = symbol c: every first-level entry says so)
+  bool flat8 = false;
+  if (MH_BATCH_FLAT8 && flavor == 2 && mx == 8u) {
+    bool ok = true;
+    for (uint32_t w = threadIdx.x; w < (uint32_t)kL1Entries; w += nthreads)
+      ok = ok && s_lut[w] == (uint16_t)((((w >> (kLutBits - 8)) << 8) - 8u) & 0xFFFFu);
+    flat8 = __syncthreads_and(ok);
+  }
+  if (flat8)
+    flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc);
+  else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
     batch_loop<kDelta, Lut13Flat>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);

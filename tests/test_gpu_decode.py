@@ -342,6 +342,59 @@ def test_batch_kernel_flat_table(mh, oracle, device):
     assert np.array_equal(out[3], _oracle_decode(oracle, efs[3]))
 
 
+def _shift_stream(ef, k: int):
+    """The same frame with its code stream moved k bits later (k leading zero bits) and
+    every block offset with it: blocks off the byte grid, which no reference producer
+    writes but the buffer contract allows."""
+    import dataclasses
+    from metalhuffman_amd import _native as N
+    bits = np.unpackbits(ef.codes[: ef.payload_bytes])
+    moved = np.packbits(np.concatenate([np.zeros(k, np.uint8), bits]))
+    codes = np.concatenate([moved, np.zeros(N.MH_CODES_PAD, np.uint8)])
+    return dataclasses.replace(ef, codes=codes, block_offsets=(ef.block_offsets + np.uint32(k)).astype(np.uint32))
+
+
+@pytest.mark.parametrize("fmt", ["delta", "no_delta", "block_init", "edges", "flat4", "off_grid"])
+def test_batch_kernel_flat8_path(mh, oracle, device, fmt):
+    """Flat 8-bit tables (uniform bytes: every code 8 bits, code c = symbol c) take the
+    batch kernel's byte-arithmetic path; 5 frames = 1,280+ tiles per launch (batch
+    kernel). Formats: delta, raw symbols, per-block init bytes (attached to flat frames:
+    the reference's init-byte producer always makes symbol 0 shorter), partial edge
+    blocks and rows past H (1032x1008 frames decoded as 1027x1001: the same block grid),
+    a flat 4-bit table (16 symbols: the general flat step), and blocks off the byte grid
+    (the general flat step, from the slow loop)."""
+    import dataclasses
+    from metalhuffman_amd import frames as F
+    kw = {}
+    if fmt == "edges":
+        base = F.uniform_random(1008, 1032, 5)
+    elif fmt == "flat4":
+        base = (F.uniform_random(1024, 1024, 6) & 15).astype(np.uint8)
+        kw = {"flags": mh.MH_FLAG_NO_DELTA}
+    else:
+        base = F.uniform_random(1024, 1024, 7)
+    if fmt == "no_delta":
+        kw = {"flags": mh.MH_FLAG_NO_DELTA}
+    n = 5
+    imgs = [base] + [F.block_shuffle(base, 700 + s) for s in range(1, n)]
+    efs = [mh.encode_frame(im, **kw) for im in imgs]
+    L = efs[0].canon[efs[0].canon > 0]
+    assert L.min() == L.max() == (4 if fmt == "flat4" else 8), (L.min(), L.max())
+    if fmt == "off_grid":
+        efs = [_shift_stream(ef, 3 + i) for i, ef in enumerate(efs)]
+    elif fmt == "block_init":
+        r = np.random.default_rng(8)
+        efs = [dataclasses.replace(ef, block_init=r.integers(0, 256, ef.n_blocks, dtype=np.uint8)) for ef in efs]
+    elif fmt == "edges":
+        efs = [dataclasses.replace(ef, width=1027, height=1001) for ef in efs]
+        imgs = [im[:1001, :1027] for im in imgs]
+    out = _decode(efs, device)
+    for i, (im, ef) in enumerate(zip(imgs, efs)):
+        if fmt != "block_init":
+            assert np.array_equal(out[i], im), i
+        assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
+
+
 @pytest.mark.parametrize("kind", ["flat", "noesc", "general"])
 def test_batch_kernel_multi_tile_waves_per_flavour(mh, device, bigbridge, kind):
     """Every step flavour of the batch kernel (one persistent-loop instantiation each)
