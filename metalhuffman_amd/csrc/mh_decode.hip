@@ -171,6 +171,13 @@ __device__ __forceinline__ uint32_t pack_prev4(uint32_t a, uint32_t b, uint32_t 
   return lo | hi;
 }
 
+// byte 0 of four successive sums -> one output word, 3 VALU
+__device__ __forceinline__ uint32_t pack_lo4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0400u);  // [a.0, b.0, 0, 0]
+  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000C0Cu);  // [0, 0, c.0, d.0]
+  return lo | hi;
+}
+
 // v_perm_b32 selectors: put S0.byte1 at byte J, keep S1's other bytes
 __device__ __forceinline__ constexpr uint32_t ins_sel1(int j) {
   return j == 0 ? 0x03020105u : j == 1 ? 0x03020500u : j == 2 ? 0x03050100u : 0x05020100u;
@@ -211,9 +218,10 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 //   lookup: sh >= 32 drops a word, sh < 32 advances by <= 16), so the chain from one
 //   lookup to the next is add, shift, and -- no compare / select on it.
 template <int kBits, bool kMaskedRefill, bool kEscapes = kBits == kLutBits, bool kSwizzle = false,
-          int kStoreAux = kBatchStoreAux, bool kLazyRefill = false>
+          int kStoreAux = kBatchStoreAux, bool kLazyRefill = false, bool kFlat8Bytes = false>
 struct StepCfg {
   static constexpr bool kLazy = kLazyRefill;
+  static constexpr bool kFlat8 = kFlat8Bytes;  // flat 8-bit canonical table: byte arithmetic
   static constexpr int kAux = kStoreAux;  // row-store cache bits
   static constexpr bool kEsc = kEscapes;
   static constexpr bool kSwz = kSwizzle;
@@ -230,6 +238,9 @@ using Lut13NoEsc = StepCfg<kLutBits, true, false>;
 // ... and for flat tables (every code the same length, e.g. uniform bytes: every
 // block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
 using Lut13Flat = StepCfg<kLutBits, true, false, true>;
+// ... and (MH_FLAT8_STAGED builds) flat 8-bit canonical tables decoded from the staged span
+// with byte arithmetic
+using Flat8Staged = StepCfg<kLutBits, true, false, false, kBatchStoreAux, false, true>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -246,6 +257,44 @@ template <bool kDelta, class Cfg, class Src>
 __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut, uint32_t p,
                                              uint32_t prev, __amdgpu_buffer_rsrc_t out,
                                              uint32_t row0, uint32_t pitch, bool dead) {
+  if constexpr (Cfg::kFlat8) {
+    // 64 one-byte codes from bit p of the staged (big-endian word) span: 17 words, each
+    // output word a 64-bit funnel shift (any bit alignment); code c is symbol c
+    typedef const __attribute__((address_space(3))) uint32_t *lds_u32;
+    typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+    const lds_u32 wp = (lds_u32)(src.w + (p >> 5) * 4u);
+    const uint32_t sh = p & 31u;
+    uint32_t w[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) w[j] = wp[j];
+    const uint32_t rbase = dead ? 0x80000000u : row0;
+    uint32_t s = prev;
+#pragma unroll
+    for (uint32_t r = 0; r < 8; ++r) {
+      uint32_t c[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t j = 2 * r + h;
+        c[h] = (uint32_t)(((((uint64_t)w[j]) << 32 | w[j + 1]) << sh) >> 32);  // big-endian: symbol 4j+i = byte 3-i
+      }
+      v2u32 v;
+      if (kDelta) {
+        uint32_t sv[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sv[i] = s = s + ((c[h] >> (24 - 8 * i)) & 0xFFu);
+          const uint32_t o = pack_lo4(sv[0], sv[1], sv[2], sv[3]);
+          if (h) v.y = o; else v.x = o;
+        }
+      } else {
+        v.x = bswap32(c[0]);
+        v.y = bswap32(c[1]);
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(v, out, (int)(rbase + r * pitch), 0, Cfg::kAux);
+    }
+    return;
+  }
   // wa: LDS address of hi's word in the staged span. An explicit local-address-space
   // pointer keeps its arithmetic 32-bit (a generic pointer was carried as a 64-bit value:
   // one 64-bit add per refill) and lets the reads fold their constant offsets.
@@ -726,14 +775,14 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 // The uniform-random 8192^2 stress frame is such a table.
 // A tile with a block that does not start on a byte (no reference producer writes one)
 // takes the general flat step.
-__device__ __forceinline__ uint32_t pack_lo4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0400u);  // [a.0, b.0, 0, 0]
-  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000C0Cu);  // [0, 0, c.0, d.0]
-  return lo | hi;
-}
-
 #ifndef MH_BATCH_FLAT8           // 0: A/B builds only (the general flat step for flat 8-bit tables too)
 #define MH_BATCH_FLAT8 1
+#endif
+#ifndef MH_FLAT8_STAGED          // A/B builds only: 1 = flat 8-bit tiles through batch_loop's coalesced
+#define MH_FLAT8_STAGED 0        //    span loads and LDS stage (Flat8Staged) instead of per-lane loads
+#endif
+#ifndef MH_FLAT8_PRIO            // A/B builds only: wave priority by tiles left, as batch_loop
+#define MH_FLAT8_PRIO 0
 #endif
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
@@ -804,6 +853,9 @@ __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, u
     const Tile nxt = hdr_resolve(a, h, lane);
     flat8_issue(a, nxt, cn);
     hdr_issue(a, next_tile(a, nxt.tile, gstride), lane, h);
+#if MH_FLAT8_PRIO
+    set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
+#endif
     flat8_block<kDelta>(a, cur, lane, cc);
     cur = nxt;
     cc = cn;
@@ -909,7 +961,11 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
     flat8 = __syncthreads_and(ok);
   }
   if (flat8)
+#if MH_FLAT8_STAGED
+    batch_loop<kDelta, Flat8Staged>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
+#else
     flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc);
+#endif
   else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
