@@ -238,9 +238,6 @@ using Lut13NoEsc = StepCfg<kLutBits, true, false>;
 // ... and for flat tables (every code the same length, e.g. uniform bytes: every
 // block the same size, so lanes sit a multiple of 128 B apart): swizzled stage
 using Lut13Flat = StepCfg<kLutBits, true, false, true>;
-// ... and (MH_FLAT8_STAGED builds) flat 8-bit canonical tables decoded from the staged span
-// with byte arithmetic
-using Flat8Staged = StepCfg<kLutBits, true, false, false, kBatchStoreAux, false, true>;
 
 // One lane decodes one 8x8 block: 64 serial steps of AAPLShaders.metal:241-268
 // (cursor advance + delta fold); each finished 8-pixel block row is stored at once.
@@ -775,14 +772,8 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 // The uniform-random 8192^2 stress frame is such a table.
 // A tile with a block that does not start on a byte (no reference producer writes one)
 // takes the general flat step.
-#ifndef MH_BATCH_FLAT8           // 0: A/B builds only (the general flat step for flat 8-bit tables too)
-#define MH_BATCH_FLAT8 1
-#endif
-#ifndef MH_FLAT8_STAGED          // A/B builds only: 1 = flat 8-bit tiles through batch_loop's coalesced
-#define MH_FLAT8_STAGED 0        //    span loads and LDS stage (Flat8Staged) instead of per-lane loads
-#endif
-#ifndef MH_FLAT8_PRIO            // A/B builds only: wave priority by tiles left, as batch_loop
-#define MH_FLAT8_PRIO 0
+#ifndef MH_FLAT8                 // 0: A/B builds only (the general flat step / lookup chain for flat
+#define MH_FLAT8 1               //    8-bit tables too, in both kernels)
 #endif
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
@@ -853,9 +844,6 @@ __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, u
     const Tile nxt = hdr_resolve(a, h, lane);
     flat8_issue(a, nxt, cn);
     hdr_issue(a, next_tile(a, nxt.tile, gstride), lane, h);
-#if MH_FLAT8_PRIO
-    set_prio(min((a.total_tiles - 1u - cur.tile) / gstride, 3u));
-#endif
     flat8_block<kDelta>(a, cur, lane, cc);
     cur = nxt;
     cc = cn;
@@ -954,18 +942,14 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
   // flat 8-bit and canonical (code c = symbol c: every first-level entry says so)
   bool flat8 = false;
-  if (MH_BATCH_FLAT8 && flavor == 2 && mx == 8u) {
+  if (MH_FLAT8 && flavor == 2 && mx == 8u) {
     bool ok = true;
     for (uint32_t w = threadIdx.x; w < (uint32_t)kL1Entries; w += nthreads)
       ok = ok && s_lut[w] == (uint16_t)((((w >> (kLutBits - 8)) << 8) - 8u) & 0xFFFFu);
     flat8 = __syncthreads_and(ok);
   }
   if (flat8)
-#if MH_FLAT8_STAGED
-    batch_loop<kDelta, Flat8Staged>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
-#else
     flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc);
-#endif
   else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
@@ -998,6 +982,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 #define MH_SMALL_WAVES 4
 #endif
 constexpr int kSmallWaves = MH_SMALL_WAVES;  // waves per workgroup (one tile each)
+static_assert(kSmallWaves * 64 >= 256, "the flat 8-bit check gives each of the 256 prefixes a thread");
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
@@ -1029,7 +1014,9 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
 #endif
   MH_STAMP(0);
 
-  const uint32_t max_len = *reinterpret_cast<const uint32_t *>(prepared + kMaxLenOff);  // scalar load
+  typedef unsigned int v2u32s __attribute__((ext_vector_type(2)));
+  const v2u32s lens = *reinterpret_cast<const v2u32s *>(prepared + kMaxLenOff);  // scalar load
+  const uint32_t max_len = lens.x, min_len = lens.y;
   const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr h;
   hdr_issue(a, tile, lane, h);
@@ -1063,6 +1050,14 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   // for another wave's span (HBM, cold); each waits for its own span at its first read
   lds_barrier();
   MH_STAMP(2);
+  // a flat 8-bit canonical table (code c = symbol c, every 8-bit prefix's entry says so):
+  // byte arithmetic from the staged span instead of the lookup chain (kernel-uniform)
+  bool flat8 = false;
+  if (MH_FLAT8 && max_len == 8u && min_len == 8u) {
+    const uint32_t c = threadIdx.x;  // kSmallWaves * 64 >= 256 threads: one prefix each
+    const bool ok = c >= 256u || s_lut_small[c << (kLut14Bits - 8)] == (uint16_t)(((c << 8) - 8u) & 0xFFFFu);
+    flat8 = __syncthreads_and(ok);
+  }
   if (!live) return;  // no barrier below
   const OutTile ot = out_tile(a, t, lane);
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
@@ -1070,6 +1065,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   // the small kernel's step flavours (all with write-through row stores)
   using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux, MH_SMALL_LAZY>;
   using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux, MH_SMALL_LAZY>;
+  using SmallFlat8 = StepCfg<kLutBits, false, false, false, kSmallStoreAux, false, true>;
 #if MH_DIAG_STAMPS && MH_DIAG_CLOCK
   unsigned long long c3 = 0;
 #endif
@@ -1081,7 +1077,9 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
     c3 = __builtin_amdgcn_s_memtime();
 #endif
     LdsWords src{stage};
-    if (l14)
+    if (flat8)
+      decode_block<kDelta, SmallFlat8>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
+    else if (l14)
       decode_block<kDelta, Small14>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
     else
       decode_block<kDelta, Small13>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);

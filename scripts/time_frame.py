@@ -26,11 +26,16 @@ ap.add_argument("--k", type=int, default=200)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--batch", type=int, default=1, help="frames per launch (64: the config-4 shard)")
 ap.add_argument("--tag", default=os.path.basename(os.environ.get("MH_LIB", "default")))
+ap.add_argument("--random", action="store_true",
+                help="uniform-random 2048x1536 frames (a flat 8-bit table) instead of BigBridge shuffles")
 args = ap.parse_args()
 
 N.lib()
 bb = F.bigbridge()
-efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.frames)]
+if args.random:
+    efs = [mh.encode_frame(F.uniform_random(1536, 2048, 4000 + i)) for i in range(args.frames)]
+else:
+    efs = [mh.encode_frame(F.block_shuffle(bb, i) if i else bb) for i in range(args.frames)]
 t1, t2 = efs[0].tables()
 tabs = D.DeviceTables.upload(t1, t2, "cuda")
 if args.batch > 1:

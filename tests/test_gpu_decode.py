@@ -354,11 +354,13 @@ def _shift_stream(ef, k: int):
     return dataclasses.replace(ef, codes=codes, block_offsets=(ef.block_offsets + np.uint32(k)).astype(np.uint32))
 
 
+@pytest.mark.parametrize("n", [1, 5])
 @pytest.mark.parametrize("fmt", ["delta", "no_delta", "block_init", "edges", "flat4", "off_grid"])
-def test_batch_kernel_flat8_path(mh, oracle, device, fmt):
-    """Flat 8-bit tables (uniform bytes: every code 8 bits, code c = symbol c) take the
-    batch kernel's byte-arithmetic path; 5 frames = 1,280+ tiles per launch (batch
-    kernel). Formats: delta, raw symbols, per-block init bytes (attached to flat frames:
+def test_flat8_paths(mh, oracle, device, fmt, n):
+    """Flat 8-bit tables (uniform bytes: every code 8 bits, code c = symbol c) decode with
+    byte arithmetic instead of the lookup chain: n = 1 frame (256 tiles, the single-frame
+    kernel, from its staged span) and n = 5 frames (1,280+ tiles, the batch kernel, per-lane
+    code loads). Formats: delta, raw symbols, per-block init bytes (attached to flat frames:
     the reference's init-byte producer always makes symbol 0 shorter), partial edge
     blocks and rows past H (1032x1008 frames decoded as 1027x1001: the same block grid),
     a flat 4-bit table (16 symbols: the general flat step), and blocks off the byte grid
@@ -375,7 +377,6 @@ def test_batch_kernel_flat8_path(mh, oracle, device, fmt):
         base = F.uniform_random(1024, 1024, 7)
     if fmt == "no_delta":
         kw = {"flags": mh.MH_FLAG_NO_DELTA}
-    n = 5
     imgs = [base] + [F.block_shuffle(base, 700 + s) for s in range(1, n)]
     efs = [mh.encode_frame(im, **kw) for im in imgs]
     L = efs[0].canon[efs[0].canon > 0]
