@@ -109,3 +109,20 @@ def test_container_header_matches_reference_encoder(mh):
         assert mh.Huffman.parseContainerHeader(hdr) == n
     with pytest.raises(mh.MHError):
         mh.Huffman.parseContainerHeader(bytes(8))
+
+
+def test_flat8_table_is_identity(mh, oracle):
+    """The premise of the decoders' flat 8-bit path (mh_decode.hip flat8_*): when every
+    code is 8 bits (all 256 symbols, e.g. uniform bytes), canonical assignment gives
+    symbol c the code c, so T1 entry c is (symbol c, 8 bits) -- in the product's tables and
+    in the oracle's restatement of HuffmanUtil.cpp's split tables alike."""
+    from metalhuffman_amd import frames as F
+    from metalhuffman_amd.codec import Huffman
+    for h, w, seed in [(256, 256, 1), (64, 512, 2), (1024, 256, 3)]:
+        ef = mh.encode_frame(F.uniform_random(h, w, seed))
+        assert ef.canon.min() == ef.canon.max() == 8
+        t1, t2 = Huffman.generateSplitLookupTables(ef.canon)
+        o1, _ = oracle.split_tables(ef.canon)
+        assert np.array_equal(t1, o1)
+        pairs = t1.reshape(256, 2)
+        assert np.array_equal(pairs[:, 0], np.arange(256)) and (pairs[:, 1] == 8).all()
