@@ -775,6 +775,10 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 #ifndef MH_FLAT8                 // 0: A/B builds only (the general flat step / lookup chain for flat
 #define MH_FLAT8 1               //    8-bit tables too, in both kernels)
 #endif
+#ifndef MH_FLAT8_STORE_AUX       // A/B builds only: the flat 8-bit path's row-store cache bits
+#define MH_FLAT8_STORE_AUX 2
+#endif
+constexpr int kFlat8StoreAux = MH_FLAT8_STORE_AUX;
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
 };
@@ -801,7 +805,7 @@ __device__ __forceinline__ void flat8_block(const DecodeArgs &a, const Tile &t, 
   typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
   const uint32_t sb = (t.start + (t.p >> 3)) & 3u;
   const OutTile ot = out_tile(a, t, lane);
-  const uint32_t rbase = t.valid ? ot.row0 : 0x80000000u;
+  const uint32_t rbase = (t.valid && !MH_DIAG_DROP_STORES) ? ot.row0 : 0x80000000u;
   const uint32_t pitch = (uint32_t)a.out_pitch;
   uint32_t s = t.init;  // running delta sum (byte 0)
 #pragma unroll
@@ -822,7 +826,7 @@ __device__ __forceinline__ void flat8_block(const DecodeArgs &a, const Tile &t, 
       v.x = c0;
       v.y = c1;
     }
-    __builtin_amdgcn_raw_buffer_store_b64(v, ot.rsrc, (int)(rbase + r * pitch), 0, kBatchStoreAux);
+    __builtin_amdgcn_raw_buffer_store_b64(v, ot.rsrc, (int)(rbase + r * pitch), 0, kFlat8StoreAux);
   }
 }
 
