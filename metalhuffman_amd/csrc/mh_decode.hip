@@ -775,13 +775,6 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 #ifndef MH_FLAT8                 // 0: A/B builds only (the general flat step / lookup chain for flat
 #define MH_FLAT8 1               //    8-bit tables too, in both kernels)
 #endif
-#ifndef MH_FLAT8_GROUP           // A/B builds only: > 1 = tiles per round trip (flat8_loop_grouped)
-#define MH_FLAT8_GROUP 1
-#endif
-#ifndef MH_FLAT8_STORE_AUX       // A/B builds only: the flat 8-bit path's row-store cache bits
-#define MH_FLAT8_STORE_AUX 2
-#endif
-constexpr int kFlat8StoreAux = MH_FLAT8_STORE_AUX;
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
 };
@@ -829,7 +822,7 @@ __device__ __forceinline__ void flat8_block(const DecodeArgs &a, const Tile &t, 
       v.x = c0;
       v.y = c1;
     }
-    __builtin_amdgcn_raw_buffer_store_b64(v, ot.rsrc, (int)(rbase + r * pitch), 0, kFlat8StoreAux);
+    __builtin_amdgcn_raw_buffer_store_b64(v, ot.rsrc, (int)(rbase + r * pitch), 0, kBatchStoreAux);
   }
 }
 
@@ -863,56 +856,6 @@ __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, u
     const Tile tt = hdr_resolve(a, hs, lane);
     const OutTile ot = out_tile(a, tt, lane);
     decode_halves<kDelta, Lut13Flat>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
-  }
-}
-
-// Grouped variant (MH_FLAT8_GROUP = G > 1, A/B builds): G tiles per round trip. The
-// headers of a group are resolved together, then all G tiles' codes are issued at once
-// with the next group's headers behind them, so a wave pays one header round trip plus
-// one codes round trip per group instead of one (codes + next header) per tile.
-template <bool kDelta, int G>
-__device__ __forceinline__ void flat8_loop_grouped(const DecodeArgs &a, uint32_t lane, uint8_t *stage,
-                                                   const uint8_t *lut, uint32_t t0, uint32_t gstride,
-                                                   const TileHdr &hc) {
-  TileHdr h[G];
-  uint32_t t[G];
-  h[0] = hc;
-  t[0] = t0;
-#pragma unroll
-  for (int g = 1; g < G; ++g) {
-    t[g] = next_tile(a, t[g - 1], gstride);
-    hdr_issue(a, t[g], lane, h[g]);
-  }
-  while (t[0] < a.total_tiles) {  // wave-uniform
-    Tile c[G];
-    bool off_grid = false;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      c[g] = hdr_resolve(a, h[g], lane);
-      off_grid = off_grid || (c[g].tile < a.total_tiles && c[g].valid && (c[g].p & 7u) != 0u);
-    }
-    if (__builtin_expect(__ballot(off_grid) != 0, 0)) break;
-    Flat8Codes x[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) flat8_issue(a, c[g], x[g]);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      t[g] = next_tile(a, g ? t[g - 1] : t[G - 1], gstride);
-      hdr_issue(a, t[g], lane, h[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (c[g].tile < a.total_tiles) flat8_block<kDelta>(a, c[g], lane, x[g]);
-  }
-  // Slow loop (no reference producer gets here): the general flat step, no prefetch, from
-  // the first tile of the group that held an off-grid block.
-  for (uint32_t tt = t[0]; tt < a.total_tiles; tt = next_tile(a, tt, gstride)) {
-    __builtin_amdgcn_s_waitcnt(0);
-    TileHdr hs;
-    hdr_issue(a, tt, lane, hs);
-    const Tile ts = hdr_resolve(a, hs, lane);
-    const OutTile ot = out_tile(a, ts, lane);
-    decode_halves<kDelta, Lut13Flat>(a, ts, lane, lut, stage, ot.rsrc, ot.row0, !ts.valid);
   }
 }
 
@@ -1006,11 +949,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
     flat8 = __syncthreads_and(ok);
   }
   if (flat8)
-#if MH_FLAT8_GROUP > 1
-    flat8_loop_grouped<kDelta, MH_FLAT8_GROUP>(a, lane, stage, lut, t0, gstride, hc);
-#else
     flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc);
-#endif
   else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
