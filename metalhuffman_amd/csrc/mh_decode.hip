@@ -39,9 +39,6 @@ namespace {
 #ifndef MH_DIAG_CLOCK           // diagnostic builds only: core-clock cycles of the single-frame
 #define MH_DIAG_CLOCK 0         //    decode in stamp slot 5 (scripts/diag_stamps.py --clock)
 #endif
-#ifndef MH_SMALL_LAZY_BCAST     // A/B builds only: 1 = the lazy step's next-word read goes to one
-#define MH_SMALL_LAZY_BCAST 0   //    shared dword for lanes that did not refill
-#endif
 #ifndef MH_DIAG_DROP_STORES     // diagnostic builds only: every row store out of range (dropped)
 #define MH_DIAG_DROP_STORES 0
 #endif
@@ -317,10 +314,6 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   uint32_t hi = rd(wa);
   uint32_t lo = rd(wa + 4);
   uint32_t nw = rd(wa + 8);
-  uint32_t nwv = 0;    // MH_SMALL_LAZY_BCAST: the last step's next-word read ...
-  bool nwc = false;    // ... and whether that step refilled
-  (void)nwv;
-  (void)nwc;
 
   // sh <= 47 at every lookup keeps >= 16 valid window bits.
 #define MH_LOOKUP(A1)                                                               \
@@ -371,9 +364,6 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
   {                                                                                 \
     const uint64_t x = (((uint64_t)hi) << 32) | lo;                                 \
     MH_LOOKUP((uint32_t)(x >> (S & 63u)) & Cfg::kMask)                              \
-    /* broadcast variant: last step's read, landed by now (no refill follows a */   \
-    /* refill, so a refilling step never needs the read of the step before)     */  \
-    if constexpr (MH_SMALL_LAZY_BCAST) nw = nwc ? nwv : nw;                          \
     /* off the chain: refill from the cursor this lookup used */                    \
     const bool c = (S & 0xFFu) <= kRefill;                                         \
     hi = c ? lo : hi;                                                               \
@@ -384,14 +374,7 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     /* keep S + d*8 one add ahead of S + e (else it is re-associated onto the  */  \
     /* chain), and the selects as selects                                       */  \
     asm volatile("" : "+v"(S), "+v"(hi), "+v"(lo));                                \
-    if constexpr (MH_SMALL_LAZY_BCAST) {                                            \
-      /* lanes that did not refill read one shared dword (a broadcast): only the */ \
-      /* refilling lanes' reads can conflict                                     */ \
-      nwv = rd(c ? wa + 8 : base);                                                  \
-      nwc = c;                                                                      \
-    } else {                                                                        \
-      nw = rd(wa + 8);                                                              \
-    }                                                                               \
+    nw = rd(wa + 8);                                                                \
     MH_FINISH(J, OW)                                                                \
   }
 #define MH_STEP_R(J, OW)                                                            \
