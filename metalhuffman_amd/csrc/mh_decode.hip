@@ -39,9 +39,6 @@ namespace {
 #ifndef MH_DIAG_CLOCK           // diagnostic builds only: core-clock cycles of the single-frame
 #define MH_DIAG_CLOCK 0         //    decode in stamp slot 5 (scripts/diag_stamps.py --clock)
 #endif
-#ifndef MH_SMALL_LAZY_HALF      // A/B builds only: 1 = the lazy step reads the next word at even
-#define MH_SMALL_LAZY_HALF 0    //    steps only
-#endif
 #ifndef MH_DIAG_DROP_STORES     // diagnostic builds only: every row store out of range (dropped)
 #define MH_DIAG_DROP_STORES 0
 #endif
@@ -377,10 +374,10 @@ __device__ __forceinline__ void decode_block(const Src &src, const uint8_t *lut,
     /* keep S + d*8 one add ahead of S + e (else it is re-associated onto the  */  \
     /* chain), and the selects as selects                                       */  \
     asm volatile("" : "+v"(S), "+v"(hi), "+v"(lo));                                \
-    /* half: the next word only at even steps -- wa changes only at a refill, no */ \
+    /* the next word at even steps only: wa changes only at a refill and no     */  \
     /* refill follows a refill, so an even step lies between two refills and its */ \
-    /* read lands a step before the next one needs it                            */ \
-    if constexpr (!MH_SMALL_LAZY_HALF || ((J) & 1) == 0) nw = rd(wa + 8);         \
+    /* read lands a step before the next one needs it (half the stage reads)     */ \
+    if constexpr (((J) & 1) == 0) nw = rd(wa + 8);                                 \
     MH_FINISH(J, OW)                                                                \
   }
 #define MH_STEP_R(J, OW)                                                            \
