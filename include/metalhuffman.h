@@ -66,8 +66,9 @@ extern "C" {
 /* decode flags */
 #define MH_FLAG_NO_DELTA 0x1u    /* IMPL_DELTAS_BEFORE_HUFF_ENCODING off
                                     (AAPLShaders.metal:263-265): emit symbols raw */
-#define MH_FLAG_LANE_PAIRS 0x2u  /* diagnostic only: mh_decode returns
-                                    MH_ERR_INVALID_ARG for it. The lane-pair kernel
+#define MH_FLAG_LANE_PAIRS 0x2u  /* diagnostic only: mh_decode accepts and ignores
+                                    it (the default kernels decode; round 5 briefly
+                                    returned MH_ERR_INVALID_ARG). The lane-pair kernel
                                     (each block on two lanes -- one from the block
                                     start, one speculatively from its middle bit,
                                     re-synchronised through ds_bpermute; same output;

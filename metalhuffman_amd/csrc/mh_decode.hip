@@ -835,12 +835,18 @@ __device__ __forceinline__ void flat8_block(const DecodeArgs &a, const Tile &t, 
 // below is for a store.
 template <bool kDelta>
 __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, uint8_t *stage, const uint8_t *lut,
-                                           uint32_t t0, uint32_t gstride, const TileHdr &hc) {
+                                           uint32_t t0, uint32_t gstride, const TileHdr &hc MH_TS_PARAM) {
   TileHdr h;
   Flat8Codes cc, cn;
   Tile cur = hdr_resolve(a, hc, lane);
+  MH_STAMP(1);
   flat8_issue(a, cur, cc);
   hdr_issue(a, next_tile(a, t0, gstride), lane, h);
+#if MH_DIAG_STAMPS
+  ts[2] = ts[1];
+  ts[3] = ts[1];
+  bool first_tile = true;
+#endif
   while (cur.tile < a.total_tiles) {  // wave-uniform
     // a block off the byte grid: this tile and the rest in the slow loop below
     if (__builtin_expect(__ballot(cur.valid && ((cur.p & 7u) != 0u)) != 0, 0)) break;
@@ -848,6 +854,10 @@ __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, u
     flat8_issue(a, nxt, cn);
     hdr_issue(a, next_tile(a, nxt.tile, gstride), lane, h);
     flat8_block<kDelta>(a, cur, lane, cc);
+#if MH_DIAG_STAMPS
+    if (first_tile) MH_STAMP(4);  // the first tile's codes landed and its stores issued
+    first_tile = false;
+#endif
     cur = nxt;
     cc = cn;
   }
@@ -944,15 +954,22 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   // the escape-free flavours need a prepared table, so a full fixed copy (>= 5 waves)
   const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
   // flat 8-bit and canonical (code c = symbol c: every first-level entry says so)
+  // (16-byte reads: a chunk of 8 entries lies inside one 8-bit prefix c, every entry of it
+  // c's step word; round 5 read the entries one by one, 16 dependent reads per thread)
   bool flat8 = false;
   if (MH_FLAT8 && flavor == 2 && mx == 8u) {
     bool ok = true;
-    for (uint32_t w = threadIdx.x; w < (uint32_t)kL1Entries; w += nthreads)
-      ok = ok && s_lut[w] == (uint16_t)((((w >> (kLutBits - 8)) << 8) - 8u) & 0xFFFFu);
+    const v4u32 *q = reinterpret_cast<const v4u32 *>(s_lut);
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kL1Entries / 8u; k += nthreads) {
+      const uint32_t c = k >> (kLutBits - 8 - 3);
+      const uint32_t w = ((c << 8) - 8u) & 0xFFFFu, ww = w | (w << 16);
+      const v4u32 v = q[k];
+      ok = ok && v.x == ww && v.y == ww && v.z == ww && v.w == ww;
+    }
     flat8 = __syncthreads_and(ok);
   }
   if (flat8)
-    flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc);
+    flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc MH_TS_ARG);
   else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
   else if (flavor == 2)
@@ -1053,12 +1070,24 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   // for another wave's span (HBM, cold); each waits for its own span at its first read
   lds_barrier();
   MH_STAMP(2);
-  // a flat 8-bit canonical table (code c = symbol c, every 8-bit prefix's entry says so):
-  // byte arithmetic from the staged span instead of the lookup chain (kernel-uniform)
+  // a flat 8-bit canonical table (code c = symbol c, every entry of the staged table says
+  // so, as the batch kernel checks its whole first level): byte arithmetic from the staged
+  // span instead of the lookup chain (kernel-uniform). Thread c < 256 checks the 64 entries
+  // of prefix c, all equal to c's step word, with 8 16-byte reads.
   bool flat8 = false;
   if (MH_FLAT8 && max_len == 8u && min_len == 8u) {
     const uint32_t c = threadIdx.x;  // kSmallWaves * 64 >= 256 threads: one prefix each
-    const bool ok = c >= 256u || s_lut_small[c << (kLut14Bits - 8)] == (uint16_t)(((c << 8) - 8u) & 0xFFFFu);
+    bool ok = true;
+    if (c < 256u) {
+      const uint32_t w = ((c << 8) - 8u) & 0xFFFFu;
+      const uint32_t ww = w | (w << 16);
+      const v4u32 *q = reinterpret_cast<const v4u32 *>(s_lut_small + (c << (kLut14Bits - 8)));
+#pragma unroll
+      for (int k = 0; k < (1 << (kLut14Bits - 8)) / 8; ++k) {
+        const v4u32 v = q[k];
+        ok = ok && v.x == ww && v.y == ww && v.z == ww && v.w == ww;
+      }
+    }
     flat8 = __syncthreads_and(ok);
   }
   if (!live) return;  // no barrier below
@@ -1573,7 +1602,8 @@ int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_t
 #endif  // !MH_LANE_PAIRS
 
 // The decode entry point. The lane-pair diagnostic library exports the same body as
-// mh_diag_decode_lanepairs (and nothing else): MH_FLAG_LANE_PAIRS is honoured only there.
+// mh_diag_decode_lanepairs (and nothing else): MH_FLAG_LANE_PAIRS is honoured only there;
+// mh_decode accepts and ignores it.
 #if MH_LANE_PAIRS
 int mh_diag_decode_lanepairs(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_frame_stride,
                              void *stream) {
@@ -1584,8 +1614,9 @@ int mh_decode(const mh_frame *fr, uint8_t *d_out, size_t out_pitch, size_t out_f
   if (!fr || !d_out || !fr->d_block_offsets || !fr->d_codes || !fr->d_table1 || !fr->d_table2)
     return MH_ERR_INVALID_ARG;
   if (fr->n_frames == 0 || (fr->n_frames > 1 && !fr->d_frame_code_offsets)) return MH_ERR_INVALID_ARG;
-  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_ANY_ORDER | (MH_LANE_PAIRS ? MH_FLAG_LANE_PAIRS : 0u)))
-    return MH_ERR_INVALID_ARG;
+  // MH_FLAG_LANE_PAIRS: honoured by the diagnostic library only; the product library accepts
+  // it (callers built against round-4 libraries pass it) and decodes with the default kernels
+  if (fr->flags & ~(MH_FLAG_NO_DELTA | MH_FLAG_ANY_ORDER | MH_FLAG_LANE_PAIRS)) return MH_ERR_INVALID_ARG;
   const mh_dims &d = fr->dims;
   if (!d.width || !d.height || d.width > MH_MAX_DIM || d.height > MH_MAX_DIM ||
       d.block_width != (d.width + 7) / 8 || d.block_height != (d.height + 7) / 8)

@@ -195,7 +195,12 @@ class BatchEncoder:
 
 @dataclasses.dataclass
 class AsyncEncodedBatch:
-    """A batched encode in flight: everything on the device (per-frame slots)."""
+    """A batched encode in flight: everything on the device (per-frame slots).
+
+    Host synchronisation: frames() synchronises the stream once by default (check=True,
+    since round 5: it reads `status` and `codes_len`); a pipeline that overlaps encode with
+    decode must call frames(check=False), which stays asynchronous, and check `status`
+    itself. frame(f) always synchronises."""
     width: int
     height: int
     n_frames: int

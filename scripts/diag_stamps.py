@@ -27,6 +27,9 @@ ap.add_argument("--tag", default="")
 ap.add_argument("--clock", action="store_true",
                 help="MH_DIAG_CLOCK build: slot 5 holds the decode's core-clock cycles (s_memtime)")
 ap.add_argument("--tile8192", action="store_true", help="config 3: one 8192x8192 BigBridge mirror tile")
+ap.add_argument("--random8192", action="store_true",
+                help="config 3 stress: one 8192x8192 uniform-random frame (flat 8-bit table: the flat8 loop; "
+                     "stamps 2 and 3 = 1, stamp 4 = first tile's codes landed and stores issued)")
 ap.add_argument("--cold", action="store_true",
                 help="stamp a launch of a second, never-decoded frame set after a 1 GiB cache flush (bench.py's cold rule)")
 args = ap.parse_args()
@@ -35,7 +38,10 @@ lib = N.lib()
 if not hasattr(lib, "mh_diag_stamps"):
     sys.exit("not a MH_DIAG_STAMPS build (set MH_LIB)")
 bb = F.bigbridge()
-if args.tile8192:
+if args.random8192:
+    efs = [mh.encode_frame(F.uniform_random(8192, 8192, 1234))]
+    efs2 = [mh.encode_frame(F.block_shuffle(F.uniform_random(8192, 8192, 1234), 100))] if args.cold else efs
+elif args.tile8192:
     base = F.mirror_tile(bb, 8192, 8192)
     efs = [mh.encode_frame(base)]
     efs2 = [mh.encode_frame(F.block_shuffle(base, 100))] if args.cold else efs

@@ -69,7 +69,7 @@ def _frame(**kw):
     (dict(d_codes=None), -1),
     (dict(flags=0x80), -1),
     (dict(flags=0x8), -1),                                     # first unassigned flag bit
-    (dict(flags=0x2), -1),                                     # lane pairs: diagnostic library only
+    (dict(flags=0x2, codes_bytes=2), -4),                      # lane pairs: accepted (and ignored) by the product
     (dict(n_frames=0), -1),
     (dict(n_frames=2), -1),                                    # batch without frame offsets
     (dict(table2_entries=100), -5),

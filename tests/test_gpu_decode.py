@@ -396,6 +396,39 @@ def test_flat8_paths(mh, oracle, device, fmt, n):
         assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
 
 
+def test_flat8_check_reads_the_whole_prepared_table(mh, device):
+    """the flat 8-bit path must be taken only when the prepared table (a caller may
+    pass its own fr->d_lut) says code c = symbol c at EVERY entry. A table that agrees at each
+    8-bit prefix's first entry but not at one later entry of prefix 0x5A (the 13-bit first level
+    and the 14-bit table tampered alike) must send both kernels to the lookup path, which
+    decodes the tampered windows as the table says: the single-frame kernel (one frame) and the
+    batch kernel (5 frames) then write the same bytes for frame 0, and those differ from the
+    image (the tamper is live)."""
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import frames as F
+    imgs = [F.uniform_random(1024, 1024, 11)] + [F.block_shuffle(F.uniform_random(1024, 1024, 11), 900 + s)
+                                                 for s in range(4)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    lut16 = tabs.lut.view(torch.int16)
+    c, wrong = 0x5A, (((0x5A ^ 1) << 8) - 8) & 0xFFFF
+    w = torch.tensor([wrong], dtype=torch.int32, device=device).to(torch.int16)
+    lut16[(c << 5) | 1] = w[0]                      # 13-bit first level: window c:00001
+    l14 = 18464 // 2
+    lut16[l14 + ((c << 6) | 2)] = w[0]               # 14-bit table: the same windows
+    lut16[l14 + ((c << 6) | 3)] = w[0]
+    outs = []
+    for fl in (efs[:1], efs):
+        fr = D.DeviceFrames.pack(fl, device)
+        out = D.decode(fr, tabs)
+        torch.cuda.synchronize(device)
+        outs.append(out[0, :, : fr.width].cpu().numpy())
+    assert not np.array_equal(outs[0], imgs[0])
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("kind", ["flat", "noesc", "general"])
 def test_batch_kernel_multi_tile_waves_per_flavour(mh, device, bigbridge, kind):
     """Every step flavour of the batch kernel (one persistent-loop instantiation each)
