@@ -50,15 +50,10 @@ constexpr int kMaxWavesPerWG = 8;             // batch kernel workgroup width
 constexpr int kMinWavesPerEU = 6;             // register cap: 6 waves/SIMD = what the LDS budget admits
 // Row-store cache bits (gfx950 aux field: 1 sc0, 2 nt, 16 sc1). Batch kernel: nt.
 // Small-launch kernel: nt sc1, write-through, so nothing dirty is left in the XCDs'
-// L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt).
-#ifndef MH_BATCH_STORE_AUX      // A/B builds only
-#define MH_BATCH_STORE_AUX 2
-#endif
-constexpr int kBatchStoreAux = MH_BATCH_STORE_AUX;
-#ifndef MH_SMALL_STORE_AUX      // A/B builds only
-#define MH_SMALL_STORE_AUX 18
-#endif
-constexpr int kSmallStoreAux = MH_SMALL_STORE_AUX;
+// L2s for the end-of-kernel release to write back (profiles/r03_v5_store_write_through_ab.txt;
+// both re-checked cold in round 5: profiles/r05_batch_store_policy_ab.txt, r05_small_store_policy_ab.txt).
+constexpr int kBatchStoreAux = 2;
+constexpr int kSmallStoreAux = 18;
 static_assert(kStageBytes % 16 == 0, "stage uses 16-byte chunks");
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
@@ -214,7 +209,8 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 // kMasked: only the lanes that consumed a word read the next one (batch kernel);
 //   the small-launch kernel's latency-bound chain reads unmasked.
 // kLazy: the refill test runs at every step on the cursor the lookup itself uses, in the
-//   lookup's LDS shadow, and takes effect at the next step (sh <= 47 still holds at every
+//   lookup's LDS shadow, and takes effect at the next step (the small kernel's step since
+//   round 5: profiles/r05_lazy_ab.txt) (sh <= 47 still holds at every
 //   lookup: sh >= 32 drops a word, sh < 32 advances by <= 16), so the chain from one
 //   lookup to the next is add, shift, and -- no compare / select on it.
 template <int kBits, bool kMaskedRefill, bool kEscapes = kBits == kLutBits, bool kSwizzle = false,
@@ -774,10 +770,8 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 // by v_alignbyte, one SDWA byte add per symbol for the delta sum, 3 VALU per output word.
 // The uniform-random 8192^2 stress frame is such a table.
 // A tile with a block that does not start on a byte (no reference producer writes one)
-// takes the general flat step.
-#ifndef MH_FLAT8                 // 0: A/B builds only (the general flat step / lookup chain for flat
-#define MH_FLAT8 1               //    8-bit tables too, in both kernels)
-#endif
+// takes the general flat step. (Both kernels; the lookup chain for flat tables is the
+// round-5 A/B baseline: profiles/r05_flat8_ab.txt, r05_flat8_small_ab.txt.)
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
 };
@@ -957,7 +951,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   // (16-byte reads: a chunk of 8 entries lies inside one 8-bit prefix c, every entry of it
   // c's step word; round 5 read the entries one by one, 16 dependent reads per thread)
   bool flat8 = false;
-  if (MH_FLAT8 && flavor == 2 && mx == 8u) {
+  if (flavor == 2 && mx == 8u) {
     bool ok = true;
     const v4u32 *q = reinterpret_cast<const v4u32 *>(s_lut);
     for (uint32_t k = threadIdx.x; k < (uint32_t)kL1Entries / 8u; k += nthreads) {
@@ -995,13 +989,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 // single-level 14-bit table drops the escape test. Workgroups of 4 waves (one per
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
-#ifndef MH_SMALL_LAZY           // 1: lazy refill in the small kernel's steps (0: A/B builds only;
-#define MH_SMALL_LAZY 1         //    profiles/r05_lazy_ab.txt)
-#endif
-#ifndef MH_SMALL_WAVES          // A/B builds only
-#define MH_SMALL_WAVES 4
-#endif
-constexpr int kSmallWaves = MH_SMALL_WAVES;  // waves per workgroup (one tile each)
+constexpr int kSmallWaves = 4;  // waves per workgroup (one tile each)
 static_assert(kSmallWaves * 64 >= 256, "the flat 8-bit check gives each of the 256 prefixes a thread");
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
@@ -1075,7 +1063,7 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   // span instead of the lookup chain (kernel-uniform). Thread c < 256 checks the 64 entries
   // of prefix c, all equal to c's step word, with 8 16-byte reads.
   bool flat8 = false;
-  if (MH_FLAT8 && max_len == 8u && min_len == 8u) {
+  if (max_len == 8u && min_len == 8u) {
     const uint32_t c = threadIdx.x;  // kSmallWaves * 64 >= 256 threads: one prefix each
     bool ok = true;
     if (c < 256u) {
@@ -1095,8 +1083,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
   const uint32_t row0 = ot.row0;
   // the small kernel's step flavours (all with write-through row stores)
-  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux, MH_SMALL_LAZY>;
-  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux, MH_SMALL_LAZY>;
+  using Small14 = StepCfg<kLut14Bits, false, false, false, kSmallStoreAux, true>;
+  using Small13 = StepCfg<kLutBits, false, true, false, kSmallStoreAux, true>;
   using SmallFlat8 = StepCfg<kLutBits, false, false, false, kSmallStoreAux, false, true>;
 #if MH_DIAG_STAMPS && MH_DIAG_CLOCK
   unsigned long long c3 = 0;

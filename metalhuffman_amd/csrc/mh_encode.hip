@@ -180,11 +180,8 @@ static_assert(kTileGroups <= kSplitBatch && kCodeTile % 32 == 0, "a split workgr
 // 256 (round 5) halves round 4's per-tile records (counts, offsets, last-block symbols)
 // that the split writes and the trees read: 64 BigBridge shuffles per call, 571 -> 557 MB
 // of HBM traffic and 3.02-3.07 -> 2.88-2.93 us per frame (profiles/r05_encoder_batch_ab.txt).
-// A/B builds set MH_BATCH_TILE.
-#ifndef MH_BATCH_TILE
-#define MH_BATCH_TILE 256
-#endif
-constexpr uint32_t kBatchTile = MH_BATCH_TILE;
+// (128 and 512 measured beside it: the same file.)
+constexpr uint32_t kBatchTile = 256;
 static_assert(kBatchTile / 32 <= 2 * kSplitBatch && kBatchTile % 32 == 0 && kBatchTile * 64 < 65536,
               "a split workgroup loads a batch tile's rows at once; u16 tile counts");
 
