@@ -85,6 +85,17 @@ def test_no_shift_amount_in_last_vgpr(mh):
     assert not bad, bad[:8]
 
 
+def test_diagnostic_libraries_no_shift_amount_in_last_vgpr(mh):
+    """The same guard on the diagnostic libraries the GPU tests load (lane pairs, spin-0)."""
+    import metalhuffman_amd.build as B
+    B.build_diag()
+    for name in B.DIAG_LIBS:
+        path = B.diag_lib_path(name)
+        ks = _kernels(path)
+        bad = high_reg_shifts(_disasm(path), {k: v[3] for k, v in ks.items()})
+        assert not bad, (name, bad[:8])
+
+
 def _kernels(lib_path):
     objdump, readelf = os.path.join(LLVM, "llvm-objdump"), os.path.join(LLVM, "llvm-readelf")
     if not (os.path.exists(objdump) and os.path.exists(readelf)):
