@@ -119,6 +119,18 @@ def ensure_objects(force: bool = False, verbose: bool = False, only=None) -> lis
     return objs
 
 
+def _guard(lib: str) -> None:
+    """Refuse to install a library whose code objects fail isa_guard.check_library (a 64-bit
+    shift amount in a kernel's last VGPR -- round 5's miscompute -- or a spill)."""
+    from . import isa_guard
+    if not isa_guard.available():
+        print(f"warning: {isa_guard.LLVM} missing, ISA guard skipped for {lib}", file=sys.stderr)
+        return
+    problems = isa_guard.check_library(lib)
+    if problems:
+        raise RuntimeError(f"ISA guard refused {lib} (left in place for inspection):\n  " + "\n  ".join(problems))
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Rebuild by CONTENT, not mtime (a snapshot may carry any mtimes), and link the
     library with its stamp compiled in, so the loader can refuse a stale one.
@@ -144,6 +156,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(full), flush=True)
         subprocess.run(full, check=True)
+        _guard(tmp)
         os.replace(tmp, LIB)  # never rewrite a mapped library in place
         _write_stamp(LIB, lst)
     return LIB
@@ -205,6 +218,7 @@ def build_diag(force: bool = False, verbose: bool = False) -> list[str]:
             f.write(f'const char* mh_build_stamp(void) {{ return "diag:{name}:{stamp}"; }}\n')
         subprocess.run(["gcc", "-O2", "-fPIC", "-c", stamp_c, "-o", stamp_c[:-1] + "o"], check=True)
         subprocess.run([HIPCC, *LINK_FLAGS, "-o", lib + ".tmp"] + objs + [stamp_c[:-1] + "o"], check=True)
+        _guard(lib + ".tmp")
         os.replace(lib + ".tmp", lib)
         _write_stamp(lib, stamp)
     return out

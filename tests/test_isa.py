@@ -8,46 +8,23 @@
    with only that amount moved to another VGPR decoded every tile right, and an s_nop in
    front did not help (profiles/r06_forensic_isa_patch.txt). LLVM guards this pattern for
    gfx90a only (GCNHazardRecognizer::fixShift64HighRegBug), so nothing in hipcc's gfx950
-   output rules it out: this test does.
+   output rules it out: this test does, and build() runs the same check (metalhuffman_amd/isa_guard.py)
+   before it installs a library.
 2. No kernel spills registers or uses scratch: the kernels' register budget is part of
    their design, so a spill is a build failure, not a slow path.
    (Round 5's failing build also spilled; a spill is what filled v79 there.)"""
 from __future__ import annotations
 
-import os
-import re
-import shutil
-import subprocess
-import tempfile
-
 import pytest
 
-LLVM = "/opt/rocm/lib/llvm/bin"
+from metalhuffman_amd.isa_guard import check_library, high_reg_shifts
 
 
-_SHIFT64 = re.compile(r"\b(v_lshlrev_b64|v_lshrrev_b64|v_ashrrev_i64)(?:_e64)?\s+v\[\d+:\d+\],\s*v(\d+)\b")
-
-
-def high_reg_shifts(disasm: str, vgpr_count: dict) -> list:
-    """(kernel, instruction) pairs whose 64-bit shift amount is the last VGPR of the kernel's
-    8-register allocation granule with the next VGPR unallocated (vgpr_count: kernel symbol
-    -> .vgpr_count; functions not in it are skipped)."""
-    bad, cur, alloc = [], None, 0
-    for line in disasm.splitlines():
-        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
-        if m:
-            cur = m.group(1)
-            n = vgpr_count.get(cur)
-            alloc = (n + 7) // 8 * 8 if n is not None else 0
-            continue
-        if cur is None or not alloc:
-            continue
-        m = _SHIFT64.search(line)
-        if m:
-            r = int(m.group(2))
-            if r % 8 == 7 and r + 1 >= alloc:
-                bad.append((cur, line.strip()))
-    return bad
+def _tools():
+    from metalhuffman_amd import isa_guard
+    if not isa_guard.available():
+        pytest.skip("ROCm llvm tools not found")
+    return isa_guard
 
 
 def test_high_reg_shift_checker():
@@ -64,17 +41,7 @@ def test_high_reg_shift_checker():
 
 
 def _disasm(lib_path):
-    objdump = os.path.join(LLVM, "llvm-objdump")
-    if not os.path.exists(objdump):
-        pytest.skip("ROCm llvm tools not found")
-    with tempfile.TemporaryDirectory() as d:
-        lib = os.path.join(d, os.path.basename(lib_path))
-        shutil.copy(lib_path, lib)
-        subprocess.run([objdump, "--offloading", lib], cwd=d, check=True, capture_output=True)
-        cos = [f for f in os.listdir(d) if "amdgcn-amd-amdhsa--gfx950" in f]
-        assert cos, os.listdir(d)
-        return "\n".join(subprocess.run([objdump, "-d", "--mcpu=gfx950", os.path.join(d, co)], check=True,
-                                        capture_output=True, text=True).stdout for co in cos)
+    return _tools().disasm(lib_path)
 
 
 def test_no_shift_amount_in_last_vgpr(mh):
@@ -97,27 +64,7 @@ def test_diagnostic_libraries_no_shift_amount_in_last_vgpr(mh):
 
 
 def _kernels(lib_path):
-    objdump, readelf = os.path.join(LLVM, "llvm-objdump"), os.path.join(LLVM, "llvm-readelf")
-    if not (os.path.exists(objdump) and os.path.exists(readelf)):
-        pytest.skip("ROCm llvm tools not found")
-    out = {}
-    with tempfile.TemporaryDirectory() as d:
-        lib = os.path.join(d, os.path.basename(lib_path))
-        shutil.copy(lib_path, lib)
-        subprocess.run([objdump, "--offloading", lib], cwd=d, check=True, capture_output=True)
-        cos = [f for f in os.listdir(d) if "amdgcn-amd-amdhsa--gfx950" in f]
-        assert cos, os.listdir(d)
-        for co in cos:
-            notes = subprocess.run([readelf, "--notes", os.path.join(d, co)], check=True, capture_output=True,
-                                   text=True).stdout
-            for blk in re.split(r"\n\s+- \.", notes):
-                m = re.search(r"\.name:\s+(\S+)", blk)
-                if not m or "kernel" not in m.group(1):
-                    continue
-                get = lambda k: int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))
-                out[m.group(1)] = (get("private_segment_fixed_size"), get("vgpr_spill_count"),
-                                   get("sgpr_spill_count"), get("vgpr_count"))
-    return out
+    return _tools().kernels(lib_path)
 
 
 def test_product_kernels_do_not_spill(mh):
@@ -132,3 +79,11 @@ def test_product_kernels_do_not_spill(mh):
     for k, v in ks.items():
         if "mh_decode_kernel" in k:
             assert v[3] <= 80, (k, v)
+
+
+def test_build_guard_passes_product_and_diag(mh):
+    """The check build() runs before installing a library finds nothing in the shipped ones."""
+    import metalhuffman_amd.build as B
+    _tools()
+    for path in [mh.LIB_PATH] + B.build_diag():
+        assert check_library(path) == [], path
