@@ -161,7 +161,10 @@ size_t mh_lut_bytes(void);
 
 /* Derive the decoder's 2^MH_LUT_BITS-entry first-level table from T1/T2 on the
  * device (one small kernel). Rebuild only when the tables change, exactly as
- * the reference builds T1/T2 once (AAPLRenderer.m:608). */
+ * the reference builds T1/T2 once (AAPLRenderer.m:608). The buffer is opaque:
+ * write it only through mh_prepare_lut or mh_build_tables_device -- besides the
+ * entries it carries facts derived from them (longest / shortest code, whether
+ * the code is the identity 8-bit code) that the decode kernels act on. */
 int mh_prepare_lut(const mh_lookup_symbol *d_table1, const mh_lookup_symbol *d_table2,
                    uint32_t table2_entries, uint16_t *d_lut, void *stream);
 

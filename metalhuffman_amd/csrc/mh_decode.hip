@@ -140,7 +140,7 @@ __device__ void build_lut(const uint16_t *t1, const uint16_t *t2, uint32_t t2_en
 __global__ void __launch_bounds__(1024) mh_prepare_lut_kernel(const uint16_t *t1, const uint16_t *t2,
                                                               uint32_t t2_entries, uint8_t *buf) {
   __shared__ uint16_t s_t1[256];
-  __shared__ uint32_t s_scratch[3];
+  __shared__ uint32_t s_scratch[4];
   if (threadIdx.x < 256) s_t1[threadIdx.x] = t1[threadIdx.x];
   __syncthreads();
   build_prepared_lut(s_t1, t2, t2_entries, buf, s_scratch);
@@ -764,13 +764,14 @@ __device__ __forceinline__ void batch_loop(const DecodeArgs &a, uint32_t lane, u
 }
 
 // Flat 8-bit tables (every code 8 bits: all 256 symbols, canonical, so code c is symbol c
-// -- checked against the whole LDS table by the caller): a block's 64 codes are its 64
+// -- the prepared table's flat8 word, which its builder sets only when every first-level
+// entry says so, mh_lut.hpp): a block's 64 codes are its 64
 // symbol bytes, MSB-first bytes in stream order. A lane decodes its block with byte
 // arithmetic -- no table lookup and no serial bit cursor: 17 dwords of codes, realigned
 // by v_alignbyte, one SDWA byte add per symbol for the delta sum, 3 VALU per output word.
 // The uniform-random 8192^2 stress frame is such a table.
 // A tile with a block that does not start on a byte (no reference producer writes one)
-// takes the general flat step. (Both kernels; the lookup chain for flat tables is the
+// takes a staged funnel-shift step. (Both kernels; the lookup chain for flat tables is the
 // round-5 A/B baseline: profiles/r05_flat8_ab.txt, r05_flat8_small_ab.txt.)
 struct Flat8Codes {
   uint32_t w[17];  // the block's 64 code bytes from the dword below its first byte
@@ -855,14 +856,16 @@ __device__ __forceinline__ void flat8_loop(const DecodeArgs &a, uint32_t lane, u
     cur = nxt;
     cc = cn;
   }
-  // Slow loop (no reference producer gets here): the general flat step, no prefetch.
+  // Slow loop (no reference producer gets here): each half tile staged in LDS and decoded
+  // with the funnel-shift byte step (any bit alignment), no prefetch; no table needed.
+  using Batch8 = StepCfg<kLutBits, true, false, false, kBatchStoreAux, false, true>;
   for (uint32_t t = cur.tile; t < a.total_tiles; t = next_tile(a, t, gstride)) {
     __builtin_amdgcn_s_waitcnt(0);
     TileHdr hs;
     hdr_issue(a, t, lane, hs);
     const Tile tt = hdr_resolve(a, hs, lane);
     const OutTile ot = out_tile(a, tt, lane);
-    decode_halves<kDelta, Lut13Flat>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
+    decode_halves<kDelta, Batch8>(a, tt, lane, lut, stage, ot.rsrc, ot.row0, !tt.valid);
   }
 }
 
@@ -914,6 +917,13 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
   // kernel), so 4 loads per thread cover the table.
   constexpr uint32_t kLutChunks = kLutBytes / 16, kLutPer = 4;
   const bool fixed_copy = a.lut && nthreads * kLutPer >= kLutChunks;
+  // The prepared table's [longest, shortest, flat8] word (mh_lut.hpp): the oldest load of
+  // the wave (a vector load through the table's descriptor, empty without a prepared table),
+  // so it has landed by the time the table's loads have and the decisions below cost the
+  // copy no wait. (A scalar load needs a branch or a kernarg pointer to guard the no-table
+  // case, and either waits for a scalar round trip before the table's loads go out.)
+  const v4u32 lw = __builtin_amdgcn_raw_buffer_load_b128(
+      uniform_rsrc(a.lut, a.lut ? (uint32_t)kPreparedBytes : 0u), kMaxLenOff, 0, 0);
   v4u32 L[kLutPer];
   {
     const __amdgpu_buffer_rsrc_t rl = uniform_rsrc(a.lut, fixed_copy ? (uint32_t)kLutBytes : 0u);
@@ -922,24 +932,26 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
       L[k] = __builtin_amdgcn_raw_buffer_load_b128(rl, (int)((threadIdx.x + k * nthreads) * 16u), 0, 0);
   }
   hdr_issue(a, t0, lane, hc);
-  // The step flavour, from the prepared table's code lengths (kernel-uniform): issued
-  // behind the first header, so no dependent load sits in front of it.
+  // The step flavour, from the prepared table's code lengths (kernel-uniform):
   //   2: one code length (flat) -> escape-free step, swizzled stage
   //   1: no code over 13 bits   -> escape-free step
   //   0: general step (escapes), also for an in-kernel table
-  uint32_t mx = 16, mn = 0;
-  if (a.lut) {
-    const uint32_t *ml = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.lut) + kMaxLenOff);
-    mx = ml[0];
-    mn = ml[1];
-  }
+  const uint32_t mx = a.lut ? __builtin_amdgcn_readfirstlane(lw.x) : 16u;
+  const uint32_t mn = __builtin_amdgcn_readfirstlane(lw.y), f8 = __builtin_amdgcn_readfirstlane(lw.z);
+  // A flat 8-bit identity table (code c = symbol c, the prepared table's flat8 word,
+  // mh_lut.hpp) decodes by byte arithmetic with no table in LDS: no copy, no barrier. The
+  // table's loads above were issued anyway (before the word is known) and land unused.
+  // (The copy stays a block of its own in front of the flavour branch: with the branch
+  // first, the compiler hoisted the loops' common header code above it, and the table
+  // stores then waited for the header's HBM round trip -- vmcnt(0).)
+  // (The stores themselves do not wait for the word: only the barrier does.)
   if (fixed_copy) {
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
 #pragma unroll
     for (uint32_t k = 0; k < kLutPer; ++k)
       if (threadIdx.x + k * nthreads < kLutChunks) dstv[threadIdx.x + k * nthreads] = L[k];
-    lds_barrier();
-  } else if (a.lut) {
+    if (!f8) lds_barrier();
+  } else if (a.lut && !f8) {
     const v4u32 *src = reinterpret_cast<const v4u32 *>(a.lut);
     v4u32 *dstv = reinterpret_cast<v4u32 *>(s_lut);
     for (uint32_t i = threadIdx.x; i < kLutChunks; i += nthreads) dstv[i] = src[i];
@@ -947,22 +959,7 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 
   // the escape-free flavours need a prepared table, so a full fixed copy (>= 5 waves)
   const uint32_t flavor = !fixed_copy ? 0u : mx == mn ? 2u : mx <= (uint32_t)kLutBits ? 1u : 0u;
-  // flat 8-bit and canonical (code c = symbol c: every first-level entry says so)
-  // (16-byte reads: a chunk of 8 entries lies inside one 8-bit prefix c, every entry of it
-  // c's step word; round 5 read the entries one by one, 16 dependent reads per thread)
-  bool flat8 = false;
-  if (flavor == 2 && mx == 8u) {
-    bool ok = true;
-    const v4u32 *q = reinterpret_cast<const v4u32 *>(s_lut);
-    for (uint32_t k = threadIdx.x; k < (uint32_t)kL1Entries / 8u; k += nthreads) {
-      const uint32_t c = k >> (kLutBits - 8 - 3);
-      const uint32_t w = ((c << 8) - 8u) & 0xFFFFu, ww = w | (w << 16);
-      const v4u32 v = q[k];
-      ok = ok && v.x == ww && v.y == ww && v.z == ww && v.w == ww;
-    }
-    flat8 = __syncthreads_and(ok);
-  }
-  if (flat8)
+  if (f8)
     flat8_loop<kDelta>(a, lane, stage, lut, t0, gstride, hc MH_TS_ARG);
   else if (flavor == 1)
     batch_loop<kDelta, Lut13NoEsc>(a, lane, stage, lut, t0, gstride, hc, true MH_TS_ARG);
@@ -990,7 +987,6 @@ __global__ void __launch_bounds__(64 * kMaxWavesPerWG, kMinWavesPerEU) mh_decode
 // SIMD; 192 for a 2048x1536 frame) beat 8 (two waves per SIMD, fewer table copies):
 // 5.74 vs 5.89 us (profiles/r01_v15_small_step_ab.txt).
 constexpr int kSmallWaves = 4;  // waves per workgroup (one tile each)
-static_assert(kSmallWaves * 64 >= 256, "the flat 8-bit check gives each of the 256 prefixes a thread");
 constexpr int kSmallMaxTilesPerCU = 4;   // launches up to this many tiles per CU
 __shared__ __attribute__((aligned(16))) uint16_t s_lut_small[kLut14Entries];  // 14-bit, or 13-bit L1+L2
 static_assert(kLutBytes <= kLut14Bytes, "the 13-bit table fits the small kernel's LUT space");
@@ -1022,9 +1018,10 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
 #endif
   MH_STAMP(0);
 
-  typedef unsigned int v2u32s __attribute__((ext_vector_type(2)));
-  const v2u32s lens = *reinterpret_cast<const v2u32s *>(prepared + kMaxLenOff);  // scalar load
-  const uint32_t max_len = lens.x, min_len = lens.y;
+  // [longest code, shortest code, flat8] (mh_lut.hpp): one scalar load, first used behind
+  // the header's loads
+  const v4u32 lens = *reinterpret_cast<const v4u32 *>(prepared + kMaxLenOff);
+  const uint32_t max_len = lens.x;
   const uint32_t tile = min(blockIdx.x * nwaves + wave, a.total_tiles);
   TileHdr h;
   hdr_issue(a, tile, lane, h);
@@ -1055,29 +1052,15 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
     for (int k = 0; k < kLutLoads; ++k) dst[threadIdx.x + 64u * kSmallWaves * k] = L[k];
   }
   // table in LDS: an LDS-only barrier (waits lgkmcnt, not vmcnt), so no wave waits here
-  // for another wave's span (HBM, cold); each waits for its own span at its first read
+  // for another wave's span (HBM, cold); each waits for its own span at its first read.
+  // (Skipping the copy and barrier for flat tables put a branch on the lengths word in
+  // front of the header's loads, which then waited for its scalar round trip: config 2
+  // +4 %, the flat single frame gains nothing worth it.)
   lds_barrier();
   MH_STAMP(2);
-  // a flat 8-bit canonical table (code c = symbol c, every entry of the staged table says
-  // so, as the batch kernel checks its whole first level): byte arithmetic from the staged
-  // span instead of the lookup chain (kernel-uniform). Thread c < 256 checks the 64 entries
-  // of prefix c, all equal to c's step word, with 8 16-byte reads.
-  bool flat8 = false;
-  if (max_len == 8u && min_len == 8u) {
-    const uint32_t c = threadIdx.x;  // kSmallWaves * 64 >= 256 threads: one prefix each
-    bool ok = true;
-    if (c < 256u) {
-      const uint32_t w = ((c << 8) - 8u) & 0xFFFFu;
-      const uint32_t ww = w | (w << 16);
-      const v4u32 *q = reinterpret_cast<const v4u32 *>(s_lut_small + (c << (kLut14Bits - 8)));
-#pragma unroll
-      for (int k = 0; k < (1 << (kLut14Bits - 8)) / 8; ++k) {
-        const v4u32 v = q[k];
-        ok = ok && v.x == ww && v.y == ww && v.z == ww && v.w == ww;
-      }
-    }
-    flat8 = __syncthreads_and(ok);
-  }
+  // a flat 8-bit identity table (code c = symbol c; the builder sets the word only when
+  // every first-level entry says so): byte arithmetic from the staged span (kernel-uniform)
+  const bool flat8 = lens.z != 0u;
   if (!live) return;  // no barrier below
   const OutTile ot = out_tile(a, t, lane);
   const __amdgpu_buffer_rsrc_t out = ot.rsrc;
@@ -1103,6 +1086,8 @@ __global__ void __launch_bounds__(64 * kSmallWaves) mh_decode_small_kernel(
       decode_block<kDelta, Small14>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
     else
       decode_block<kDelta, Small13>(src, lut, t.p, t.init, out, row0, (uint32_t)a.out_pitch, !t.valid);
+  } else if (flat8) {
+    decode_halves<kDelta, SmallFlat8>(a, t, lane, lut, stage, out, row0, !t.valid);
   } else if (l14) {
     decode_halves<kDelta, Small14>(a, t, lane, lut, stage, out, row0, !t.valid);
   } else {

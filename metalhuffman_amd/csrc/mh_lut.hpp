@@ -22,7 +22,7 @@ constexpr int kLut14Bits = 14;
 constexpr int kLut14Entries = 1 << kLut14Bits;           // 16384 x u16
 constexpr int kLut14Off = kLutBytes;                     // byte offset in the buffer
 constexpr int kLut14Bytes = kLut14Entries * 2;           // 32768
-constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest, u32 shortest code length
+constexpr int kMaxLenOff = kLut14Off + kLut14Bytes;      // u32 longest, shortest code length, flat-8 flag
 constexpr int kPreparedBytes = kMaxLenOff + 16;          // 51248
 static_assert(kLutBytes % 16 == 0 && kLut14Bytes % 16 == 0, "lut copy uses 16-byte chunks");
 static_assert(kL2Subtables < 240, "escape entries must stay below the smallest step word");
@@ -68,13 +68,16 @@ __device__ __forceinline__ void split_lookup_batch(const uint16_t *s_t1, const u
 //     subtable, HuffmanUtil.cpp:550-556); from the first prefix P0 of a longer code
 //     on, an escape `sub` into L2[sub*8 + x] (the <= 128 long-code prefixes);
 //   the single-level 14-bit table (0 for codes over 14 bits);
-//   [longest code, shortest code, 0, 0] at kMaxLenOff.
+//   [longest code, shortest code, flat8, 0] at kMaxLenOff, flat8 = 1 when every first-level
+//     entry is the identity 8-bit code (prefix p decodes symbol p >> 5 in 8 bits: all 256
+//     symbols, code c = symbol c), the byte-arithmetic decode's condition. The decoder reads
+//     this word instead of re-checking the table at every launch.
 // Lookups go in batches of 8 with every T2 read issued before any is used.
-// `scratch`: 3 words of LDS.
+// `scratch`: 4 words of LDS.
 __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const uint16_t *t2, uint32_t t2_entries,
                                                    uint8_t *buf, uint32_t *scratch) {
   constexpr int kB = 8;
-  uint32_t &p0 = scratch[0], &mx = scratch[1], &mn = scratch[2];
+  uint32_t &p0 = scratch[0], &mx = scratch[1], &mn = scratch[2], &flat = scratch[3];
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   uint16_t *lut = reinterpret_cast<uint16_t *>(buf);
   uint16_t *lut14 = reinterpret_cast<uint16_t *>(buf + kLut14Off);
@@ -82,10 +85,11 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     p0 = (uint32_t)kL1Entries;
     mx = 0;
     mn = 255;
+    flat = 1;
   }
   __syncthreads();
   // first level of the 13-bit table and the 14-bit table
-  uint32_t my_p0 = (uint32_t)kL1Entries, my_mx = 0, my_mn = 255;
+  uint32_t my_p0 = (uint32_t)kL1Entries, my_mx = 0, my_mn = 255, my_flat = 1;
   for (uint32_t base = tid * kB; base < (uint32_t)kL1Entries; base += nt * kB) {
     uint32_t pat[kB], e[kB];
 #pragma unroll
@@ -93,8 +97,10 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     split_lookup_batch(s_t1, t2, t2_entries, pat, e);
 #pragma unroll
     for (int k = 0; k < kB; ++k) {
-      lut[base + k] = (uint16_t)step_word(e[k]);
+      const uint32_t sw = step_word(e[k]);
+      lut[base + k] = (uint16_t)sw;
       if ((e[k] >> 8) > (uint32_t)kLutBits) my_p0 = min(my_p0, base + k);
+      my_flat &= (uint32_t)(sw == (((((base + k) >> (kLutBits - 8)) << 8) - 8u) & 0xFFFFu));
     }
   }
   for (uint32_t base = tid * kB; base < (uint32_t)kLut14Entries; base += nt * kB) {
@@ -116,11 +122,13 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     my_p0 = min(my_p0, (uint32_t)__shfl_xor(my_p0, o));
     my_mx = max(my_mx, (uint32_t)__shfl_xor(my_mx, o));
     my_mn = min(my_mn, (uint32_t)__shfl_xor(my_mn, o));
+    my_flat &= (uint32_t)__shfl_xor(my_flat, o);
   }
   if ((tid & 63u) == 0) {
     atomicMin(&p0, my_p0);
     atomicMax(&mx, my_mx);
     atomicMin(&mn, my_mn);
+    if (!my_flat) flat = 0;
   }
   __syncthreads();
   // escapes and the second level (the long codes), as build_lut
@@ -135,9 +143,9 @@ __device__ __forceinline__ void build_prepared_lut(const uint16_t *s_t1, const u
     split_lookup_batch(s_t1, t2, t2_entries, pat, e);
     lut[kL1Entries + (1 << kL2Bits) + i] = (uint16_t)step_word(e[0]);
   }
-  // [longest code, shortest code, 0, 0]
+  // [longest code, shortest code, flat8, 0]
   if (tid < 4)
-    reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[tid] = tid == 0 ? mx : tid == 1 ? mn : 0u;
+    reinterpret_cast<uint32_t *>(buf + kMaxLenOff)[tid] = tid == 0 ? mx : tid == 1 ? mn : tid == 2 ? flat : 0u;
 }
 
 }  // namespace

@@ -181,8 +181,11 @@ __global__ void __launch_bounds__(1024) mh_build_tables_kernel(const uint8_t *ca
       *t2_entries = bad ? 256u : (s_ngroups + 1u) * 256u;
       if (status) *status = bad ? ((s_bad & 1u) ? MH_ERR_CODE_TOO_LONG : MH_ERR_TABLE) : MH_OK;
     }
-    if (lut && tid < 4)  // [longest code, shortest code, 0, 0]
-      reinterpret_cast<uint32_t *>(lut + kMaxLenOff)[tid] = tid == 0 ? s_mx : tid == 1 ? s_mn : 0u;
+    if (lut && tid < 4) {  // [longest code, shortest code, flat8, 0] (mh_lut.hpp)
+      // canonical codes: all 256 symbols at 8 bits is exactly the identity code c = symbol c
+      const uint32_t flat = !bad && s_wcnt[0][8] + s_wcnt[1][8] + s_wcnt[2][8] + s_wcnt[3][8] == 256u;
+      reinterpret_cast<uint32_t *>(lut + kMaxLenOff)[tid] = tid == 0 ? s_mx : tid == 1 ? s_mn : tid == 2 ? flat : 0u;
+    }
   }
   if (!lut) return;
   // this workgroup's slice of the prepared entries: L1 | L2 | the 14-bit table

@@ -396,14 +396,23 @@ def test_flat8_paths(mh, oracle, device, fmt, n):
         assert np.array_equal(out[i], _oracle_decode(oracle, ef)), i
 
 
-def test_flat8_check_reads_the_whole_prepared_table(mh, device):
-    """the flat 8-bit path must be taken only when the prepared table (a caller may
-    pass its own fr->d_lut) says code c = symbol c at EVERY entry. A table that agrees at each
-    8-bit prefix's first entry but not at one later entry of prefix 0x5A (the 13-bit first level
-    and the 14-bit table tampered alike) must send both kernels to the lookup path, which
-    decodes the tampered windows as the table says: the single-frame kernel (one frame) and the
-    batch kernel (5 frames) then write the same bytes for frame 0, and those differ from the
-    image (the tamper is live)."""
+MAXLEN_OFF = 18464 + 32768  # mh_lut.hpp kMaxLenOff: [longest, shortest, flat8, 0] (u32)
+
+
+def _lens_word(tabs):
+    return tabs.lut[MAXLEN_OFF: MAXLEN_OFF + 16].cpu().numpy().view(np.uint32).tolist()
+
+
+def test_flat8_flag_follows_every_first_level_entry(mh, oracle, device):
+    """the byte-arithmetic path is taken only for the identity 8-bit code (code c =
+    symbol c at EVERY first-level entry). Since round 6 the table builders decide it once and
+    record it in the prepared table's flat8 word (mh_lut.hpp), which both kernels read:
+    mh_prepare_lut from every first-level entry, mh_build_tables_device from the canonical
+    lengths (all 256 symbols at 8 bits). A flat 8-bit table with two symbols' codes swapped --
+    legal T1/T2 for mh_prepare_lut, every code still 8 bits -- must get flat8 = 0 and decode
+    through the lookup chain exactly as the oracle decodes it, in the single-frame kernel (one
+    frame) and the batch kernel (5 frames); 255 symbols at 8 bits (an incomplete code) gets 0
+    from both builders."""
     import torch
     from metalhuffman_amd import decoder as D
     from metalhuffman_amd import frames as F
@@ -411,22 +420,27 @@ def test_flat8_check_reads_the_whole_prepared_table(mh, device):
                                                  for s in range(4)]
     efs = [mh.encode_frame(im) for im in imgs]
     t1, t2 = efs[0].tables()
-    tabs = D.DeviceTables.upload(t1, t2, device)
-    lut16 = tabs.lut.view(torch.int16)
-    c, wrong = 0x5A, (((0x5A ^ 1) << 8) - 8) & 0xFFFF
-    w = torch.tensor([wrong], dtype=torch.int32, device=device).to(torch.int16)
-    lut16[(c << 5) | 1] = w[0]                      # 13-bit first level: window c:00001
-    l14 = 18464 // 2
-    lut16[l14 + ((c << 6) | 2)] = w[0]               # 14-bit table: the same windows
-    lut16[l14 + ((c << 6) | 3)] = w[0]
-    outs = []
+    assert _lens_word(D.DeviceTables.upload(t1, t2, device)) == [8, 8, 1, 0]
+    assert _lens_word(D.DeviceTables.from_canonical_header(efs[0].canon, device)) == [8, 8, 1, 0]
+    t1p = t1.copy()
+    t1p[2 * 0x5A], t1p[2 * 0x5B] = t1[2 * 0x5B], t1[2 * 0x5A]   # {symbol, width}: swap two symbols
+    tabs = D.DeviceTables.upload(t1p, t2, device)
+    assert _lens_word(tabs) == [8, 8, 0, 0]
     for fl in (efs[:1], efs):
         fr = D.DeviceFrames.pack(fl, device)
         out = D.decode(fr, tabs)
         torch.cuda.synchronize(device)
-        outs.append(out[0, :, : fr.width].cpu().numpy())
-    assert not np.array_equal(outs[0], imgs[0])
-    assert np.array_equal(outs[0], outs[1])
+        for i, ef in enumerate(fl):
+            want = oracle.decode_frame_shader(ef.block_offsets, ef.codes, t1p, t2, ef.width, ef.height,
+                                              block_init=ef.block_init, delta=True)
+            got = out[i, :, : fr.width].cpu().numpy()
+            assert not np.array_equal(got, imgs[i]) and np.array_equal(got, want), (len(fl), i)
+    canon = np.full(256, 8, np.uint8)
+    canon[77] = 0
+    dev = D.DeviceTables.from_canonical_header(canon, device)
+    host_t1, host_t2 = mh.codec.Huffman.generateSplitLookupTables(canon)
+    assert _lens_word(dev)[2] == 0
+    assert _lens_word(D.DeviceTables.upload(host_t1, host_t2, device))[2] == 0
 
 
 @pytest.mark.parametrize("kind", ["flat", "flat4", "noesc", "general"])
