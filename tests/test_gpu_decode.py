@@ -443,6 +443,35 @@ def test_flat8_flag_follows_every_first_level_entry(mh, oracle, device):
     assert _lens_word(D.DeviceTables.upload(host_t1, host_t2, device))[2] == 0
 
 
+def test_both_kernels_follow_the_flat8_word(mh, device):
+    """ADVICE r05's concern -- the two kernels decoding one frame differently from one prepared
+    table -- cannot arise since round 6: both act on the same flat8 word. A prepared table whose
+    entries were changed after the builder set the word (outside the contract: the buffer is
+    opaque, metalhuffman.h) decodes the same way in the single-frame kernel (one frame) and
+    the batch kernel (5 frames): by the word, i.e. the byte path, here the image."""
+    import torch
+    from metalhuffman_amd import decoder as D
+    from metalhuffman_amd import frames as F
+    imgs = [F.uniform_random(1024, 1024, 12)] + [F.block_shuffle(F.uniform_random(1024, 1024, 12), 700 + s)
+                                                 for s in range(4)]
+    efs = [mh.encode_frame(im) for im in imgs]
+    t1, t2 = efs[0].tables()
+    tabs = D.DeviceTables.upload(t1, t2, device)
+    assert _lens_word(tabs) == [8, 8, 1, 0]
+    lut16 = tabs.lut.view(torch.int16)
+    c, wrong = 0x5A, (((0x5A ^ 1) << 8) - 8) & 0xFFFF
+    w = torch.tensor([wrong], dtype=torch.int32, device=device).to(torch.int16)
+    lut16[(c << 5) | 1] = w[0]                       # 13-bit first level
+    lut16[18464 // 2 + ((c << 6) | 2)] = w[0]         # 14-bit table
+    outs = []
+    for fl in (efs[:1], efs):
+        fr = D.DeviceFrames.pack(fl, device)
+        out = D.decode(fr, tabs)
+        torch.cuda.synchronize(device)
+        outs.append(out[0, :, : fr.width].cpu().numpy())
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], imgs[0])
+
+
 @pytest.mark.parametrize("kind", ["flat", "flat4", "noesc", "general"])
 def test_batch_kernel_multi_tile_waves_per_flavour(mh, device, bigbridge, kind):
     """Every step flavour of the batch kernel (one persistent-loop instantiation each)
