@@ -45,6 +45,12 @@ constexpr uint64_t kSpinTicks = MH_DIAG_SPIN_TICKS;  // a packer's wait limit: 1
 constexpr uint32_t kCodeTile = 128;     // blocks per tile of the fused path (split + code kernels)
 constexpr uint32_t kFusedMaxTiles = 512;  // frames up to this many tiles take the two-kernel path
 
+#ifndef MH_DIAG_SPLIT_NO_HIST  // diagnostic builds only: the tiled split without its LDS histogram
+#define MH_DIAG_SPLIT_NO_HIST 0  // atomics (wrong output; the split's time without them)
+#endif
+#ifndef MH_DIAG_PACK_NO_OR  // diagnostic builds only: the batched packer without its LDS code-word
+#define MH_DIAG_PACK_NO_OR 0  // ORs (wrong output; the packer's time without them)
+#endif
 #ifndef MH_CODE_STAMPS  // diagnostic builds only: s_memrealtime phase stamps of enc_code_kernel
 #define MH_CODE_STAMPS 0
 #endif
@@ -347,7 +353,7 @@ __global__ void __launch_bounds__(256) enc_split_kernel(const uint8_t *gray, uin
       const uint64_t v = row_symbols(q[u], r, delta, block_init != nullptr, &first);
       if (block_init)  // kernel-uniform
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)first, rinit, (int)(r == 0 && b < nb32 ? b : kOob), 0, 0);
-      if (b < nb32)
+      if (!MH_DIAG_SPLIT_NO_HIST && b < nb32)
         for (int j = 0; j < 8; ++j) atomicAdd(&h[((uint32_t)(v >> (8 * j)) & 0xFFu) * kHistCopies + copy], 1u);
       vlast = v;
     }
@@ -1554,11 +1560,11 @@ __global__ void __launch_bounds__(kPackWaves * 64) enc_pack_wave_kernel(
     __builtin_amdgcn_raw_buffer_store_b32(pos + start + (r == 1 ? atot : 0u), ro, (int)(wo ? (ba + r) * 4u : kOob), 0,
                                           0);
     const uint32_t rr = pos & 31u;
-    if (on_a) {
+    if (!MH_DIAG_PACK_NO_OR && on_a) {
       or_bits(lw, rr + pa, ch[0], cl[0]);
       or_bits(lw, rr + pa + cl[0], ch[1], cl[1]);
     }
-    if (on_b) {
+    if (!MH_DIAG_PACK_NO_OR && on_b) {
       or_bits(lw, rr + pb, ch[2], cl[2]);
       or_bits(lw, rr + pb + cl[2], ch[3], cl[3]);
     }

@@ -5,6 +5,7 @@ stream; run under rocprofv3 --kernel-trace --stats for the per-kernel split
 
     python scripts/enc_batch_profile.py [n_frames] [calls]
 """
+import os
 import sys
 import time
 
@@ -25,10 +26,11 @@ g = torch.from_numpy(imgs).to(dev)
 enc = BatchEncoder(bb.shape[1], bb.shape[0], n, dev)
 a = enc.encode_async(g)
 torch.cuda.synchronize()
-assert int((a.status != 0).sum().item()) == 0
-for f in (0, n - 1):
-    ref = mh.encode_frame(imgs[f])
-    assert np.array_equal(a.frame(f).codes.cpu().numpy(), ref.codes), f
+ref = mh.encode_frame(imgs[n - 1])
+if not os.environ.get("MH_PROFILE_NO_CHECK"):  # diagnostic variants (wrong output on purpose) skip it
+    assert int((a.status != 0).sum().item()) == 0
+    for f in (0, n - 1):
+        assert np.array_equal(a.frame(f).codes.cpu().numpy(), mh.encode_frame(imgs[f]).codes), f
 alg = bb.size + ref.codes.size + 4 * ref.n_blocks  # pixels in, codes + offsets out
 print(f"alg_bytes {alg * n} per call of {n} frames")
 for rep in range(3):
